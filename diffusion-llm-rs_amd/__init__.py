@@ -1,0 +1,36 @@
+"""diffusion-llm-rs_amd: MI355X-native (gfx950) quantized inference hot path of
+zetareticula/diffusion-llm-rs.
+
+Compute runs in hand-written HIP kernels (lib/libdllm_hip.so, C-ABI in include/dllm_quant.h);
+this package is the host-side mirror of the reference's Rust operator surface:
+
+* ``quantization`` -- ``diffuse_llm_rs::quantization`` (quantize_tensor, dequantize_tensor,
+  QuantizedTensor, QuantizedKVCacheEntry) + packing.
+* ``quant``        -- the ``quantization`` crate (Quantizer, DefaultQuantizer, QuantizationType,
+  quant_utils, CalibrationData).
+* ``kvquant``      -- ``prefill_kvquant_rs::kvquant`` (BitQuantizer, PrefillKVQuant, SystemConfig)
+  and ``diffusion_prefill``'s compress/decompress_vector.
+* ``linear``       -- the int2/int4/int8 group-quantized linear layer (dequant + MFMA GEMM).
+"""
+from . import _lib
+from ._lib import (CalibrationRequired, HipError, InvalidParams, QuantizationError, ShapeMismatch,
+                   UnsupportedOperation)
+from . import quantization, quant, kvquant, linear
+from .quantization import (QuantizedKVCacheEntry, QuantizedTensor, compression_ratio, dequantize_tensor, pack,
+                           quantize_tensor, unpack)
+from .quant import CalibrationData, DefaultQuantizer, QuantizationParams, QuantizationType, quant_utils
+from .kvquant import BitQuantizer, PrefillKVQuant, SystemConfig, compress_vectors, decompress_vectors
+from .linear import MixedPrecisionStack, QuantLinear
+
+__all__ = [
+    "quantize_tensor", "dequantize_tensor", "pack", "unpack", "compression_ratio", "QuantizedTensor",
+    "QuantizedKVCacheEntry", "QuantizationType", "QuantizationParams", "DefaultQuantizer", "quant_utils",
+    "CalibrationData", "BitQuantizer", "PrefillKVQuant", "SystemConfig", "compress_vectors", "decompress_vectors",
+    "QuantLinear", "MixedPrecisionStack", "QuantizationError", "InvalidParams", "UnsupportedOperation",
+    "ShapeMismatch", "CalibrationRequired", "HipError",
+]
+
+
+def load_library():
+    """Loads the HIP library now (raises ImportError if it was not built)."""
+    return _lib.load()

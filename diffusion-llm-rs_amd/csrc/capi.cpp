@@ -1,0 +1,41 @@
+// capi.cpp -- library-level C-ABI entry points (errors, version, device probe).
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+
+#include "dllm_quant.h"
+
+namespace dllm {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string &msg) { g_last_error = msg; }
+
+int fail(int code, const std::string &msg) {
+    g_last_error = msg;
+    return code;
+}
+
+}  // namespace dllm
+
+extern "C" {
+
+const char *dllm_last_error(void) { return dllm::g_last_error.c_str(); }
+
+const char *dllm_version(void) { return "dllm_hip 0.1.0 (gfx950)"; }
+
+int dllm_device_arch(int device, char *buf, size_t len) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return dllm::fail(DLLM_ERR_NO_DEVICE, "no HIP device");
+    if (device < 0 || device >= count) return dllm::fail(DLLM_ERR_INVALID_PARAMS, "device index out of range");
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return dllm::fail(DLLM_ERR_HIP, "hipGetDeviceProperties");
+    if (buf && len) {
+        std::strncpy(buf, prop.gcnArchName, len - 1);
+        buf[len - 1] = '\0';
+    }
+    return DLLM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,82 @@
+// common.hpp -- shared helpers for the gfx950 HIP kernels and the C-ABI layer.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "dllm_quant.h"
+
+namespace dllm {
+
+// Thread-local error message behind dllm_last_error().
+void set_error(const std::string &msg);
+int fail(int code, const std::string &msg);
+
+#define DLLM_HIP_TRY(expr)                                                                        \
+    do {                                                                                          \
+        hipError_t _e = (expr);                                                                   \
+        if (_e != hipSuccess)                                                                     \
+            return ::dllm::fail(DLLM_ERR_HIP, std::string(#expr " -> ") + hipGetErrorString(_e)); \
+    } while (0)
+
+#define DLLM_LAUNCH_CHECK()                                                                       \
+    do {                                                                                          \
+        hipError_t _e = hipGetLastError();                                                        \
+        if (_e != hipSuccess)                                                                     \
+            return ::dllm::fail(DLLM_ERR_HIP, std::string("kernel launch -> ") + hipGetErrorString(_e)); \
+    } while (0)
+
+inline hipStream_t as_stream(dllm_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+constexpr int kWave = 64;      // CDNA wavefront width
+constexpr int kCUs = 256;      // MI355X compute units (8 XCDs x 32)
+constexpr int kXCDs = 8;
+
+inline unsigned grid_for(size_t work_items, int block, unsigned cap = kCUs * 8) {
+    size_t g = (work_items + block - 1) / block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return static_cast<unsigned>(g);
+}
+
+// ---- Rust f32 semantics on the device (bit-exact with the oracle) -----------------------------
+// Built with -ffp-contract=off; x/s below is the IEEE correctly rounded division (hipcc default).
+
+// `f32::clamp`: NaN passes through.  Written as compares + selects so no v_max/v_min (which
+// would drop a NaN) can be substituted.
+__device__ __forceinline__ float rs_clamp(float x, float lo, float hi) {
+    x = (x < lo) ? lo : x;
+    x = (x > hi) ? hi : x;
+    return x;
+}
+// `f as u8`: NaN -> 0, saturating, truncating.
+__device__ __forceinline__ uint32_t rs_as_u8(float f) {
+    if (!(f > 0.0f)) return 0u;          // NaN, <= 0
+    if (f >= 255.0f) return 255u;
+    return static_cast<uint32_t>(f);     // in (0, 255): truncation
+}
+// `(round(v) as i32).clamp(0, hi)` fused: NaN -> 0, saturating, then clamp.
+__device__ __forceinline__ uint32_t rs_round_i32_clamp(float v, int hi) {
+    float r = roundf(v);
+    if (!(r > 0.0f)) return 0u;          // NaN -> 0 -> 0, negatives -> 0
+    if (r >= static_cast<float>(hi)) return static_cast<uint32_t>(hi);
+    return static_cast<uint32_t>(r);
+}
+
+// Wave-level reductions (64 lanes, xor-shuffle lowers to DPP/ds_swizzle).
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+}  // namespace dllm

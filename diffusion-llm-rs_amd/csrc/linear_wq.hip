@@ -1,0 +1,540 @@
+// linear_wq.hip -- group-quantized linear layer for gfx950 (MI355X).
+//
+// Replaces SimpleDiffusionModel::forward = x.dot(W) + b (diffuse-llm-rs/src/lib.rs:806-813) with
+// W quantized per (output column n, K-group g) by quantize_tensor (quantization.rs:38-68) and
+// dequantized (quantization.rs:81-85) inside the GEMM.
+//
+// Device weight layout ("fragment-major", private to this file; canonical form is the packed
+// [K][N] bitstream of include/dllm_quant.h, converted bit-exactly in both directions):
+//   For the 32x32x16 f16 MFMA the A operand (W^ transposed: n on the lane) of lane l is
+//   W^[k = 8*(l>>5) + j][n = l&31], j = 0..7.  Per (n-tile nt of 32 columns, k64 slab) the 64
+//   lanes' codes for the slab's 4 k16-substeps are stored lane-major, `bits` 32-bit words per
+//   lane: ((nt*(K/64) + k64)*64 + lane)*bits + w.  One wave therefore fetches a slab with one
+//   fully coalesced dwordx4 (int4) / dwordx2 (int2) / 2x dwordx4 (int8) per lane.
+//   Inside a word: pair P = w*(16/bits) + p (p = 0..16/bits-1) = (substep s = P/4, v = P%4)
+//   holds fragment elements (2v, 2v+1) at bits [bits*p, ...) and [16 + bits*p, ...), so
+//   ((word >> bits*p) & mask2) | 0x64006400 is the f16 pair (1024 + q_2v, 1024 + q_2v+1).
+//   Per (group, column) one u32 `sz` = f16 pair {-(1024 + zp), f16(scale)}:
+//   f16(q - zp) is exact (|q - zp| < 2048), then one f16 rounding of (q - zp) * f16(scale).
+#include "common.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <new>
+
+typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+typedef float float16_t __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void *lds_void_ptr;
+typedef __attribute__((address_space(1))) void *gbl_void_ptr;
+
+struct dllm_linear {
+    size_t K = 0, N = 0, Npad = 0, G = 0, group = 0;
+    int bits = 0;
+    int device = 0;
+    uint32_t *wdev = nullptr;     // fragment-major words
+    uint32_t *sz = nullptr;       // [G][Npad]
+    uint32_t *canon = nullptr;    // canonical packed codes (u32-padded)
+    float *scales = nullptr;      // [G][N]
+    uint8_t *zps = nullptr;       // [G][N]
+    float *bias = nullptr;        // [Npad]
+    __half *xws = nullptr;        // f32 -> f16 staging for X
+    size_t xws_elems = 0;
+    std::mutex mu;
+};
+
+namespace dllm {
+namespace {
+
+constexpr int kBM = 256, kBN = 128, kBK = 64, kThreads = 256;
+
+inline size_t canon_words(size_t K, size_t N, int bits) { return (K * N * bits + 31) / 32; }
+
+// ---------------------------------------------------------------------------------------------
+// Weight quantization: one thread per (group g, column n).  Column reads are coalesced across
+// the wave (consecutive n).  Codes go into the canonical bitstream by atomicOr (b | 32, so no
+// code straddles a word); the buffer is zeroed first.
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) quantize_weights_kernel(const float *__restrict__ W, size_t K, size_t N,
+                                                               int bits, int group, uint32_t *__restrict__ canon,
+                                                               float *__restrict__ scales,
+                                                               uint8_t *__restrict__ zps) {
+    const size_t n = blockIdx.x * static_cast<size_t>(256) + threadIdx.x;
+    const size_t g = blockIdx.y;
+    if (n >= N) return;
+    const size_t k0 = g * group;
+    const size_t len = std::min<size_t>(group, K - k0);
+    float mx = -INFINITY, mn = INFINITY;                      // quantization.rs:41-46
+    for (size_t k = 0; k < len; ++k) { float v = W[(k0 + k) * N + n]; mx = fmaxf(mx, v); mn = fminf(mn, v); }
+    const float q_max = static_cast<float>(1u << bits) - 1.0f;
+    float scale = (mx - mn) / (q_max - 0.0f);                 // :52
+    if (scale == 0.0f) scale = 1.0f;                          // :53
+    const float zpf = 0.0f - mn / scale;                      // :55
+    const uint32_t zp = rs_as_u8(roundf(rs_clamp(zpf, 0.0f, q_max)));   // :56
+    const float zpf32 = static_cast<float>(zp);
+    scales[g * N + n] = scale;
+    zps[g * N + n] = static_cast<uint8_t>(zp);
+    const int hi = (1 << bits) - 1;
+    for (size_t k = 0; k < len; ++k) {                        // :59-65
+        float t = W[(k0 + k) * N + n] / scale;
+        t = t + zpf32;
+        const uint32_t q = rs_round_i32_clamp(t, hi);
+        const size_t bit = ((k0 + k) * N + n) * bits;
+        if (q) atomicOr(&canon[bit >> 5], q << (bit & 31));
+    }
+}
+
+__device__ __forceinline__ uint32_t canon_code(const uint32_t *__restrict__ canon, size_t k, size_t n, size_t N,
+                                               int bits) {
+    const size_t bit = (k * N + n) * bits;
+    return (canon[bit >> 5] >> (bit & 31)) & ((1u << bits) - 1u);
+}
+
+// Canonical -> fragment-major.  One thread per (column n < Npad, k64 slab); pad columns get 0.
+__global__ void __launch_bounds__(256) build_fragments_kernel(const uint32_t *__restrict__ canon, size_t K, size_t N,
+                                                              size_t Npad, int bits, uint32_t *__restrict__ wdev) {
+    const size_t n = blockIdx.x * static_cast<size_t>(256) + threadIdx.x;
+    const size_t kt = blockIdx.y;
+    if (n >= Npad) return;
+    const size_t nk = K / 64, nt = n >> 5;
+    const int pairs_per_word = 16 / bits;
+    for (int h = 0; h < 2; ++h) {
+        const size_t lane = (n & 31) + 32 * h;
+        uint32_t *dst = wdev + ((nt * nk + kt) * 64 + lane) * bits;
+        for (int w = 0; w < bits; ++w) {
+            uint32_t word = 0;
+            for (int p = 0; p < pairs_per_word; ++p) {
+                const int P = w * pairs_per_word + p, s = P >> 2, v = P & 3;
+                const size_t k = kt * 64 + s * 16 + 8 * h + 2 * v;
+                uint32_t lo = 0, hi = 0;
+                if (n < N) { lo = canon_code(canon, k, n, N, bits); hi = canon_code(canon, k + 1, n, N, bits); }
+                word |= (lo << (bits * p)) | (hi << (16 + bits * p));
+            }
+            dst[w] = word;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) build_sz_kernel(const float *__restrict__ scales, const uint8_t *__restrict__ zps,
+                                                       size_t G, size_t N, size_t Npad, uint32_t *__restrict__ sz) {
+    const size_t n = blockIdx.x * static_cast<size_t>(256) + threadIdx.x;
+    const size_t g = blockIdx.y;
+    if (n >= Npad) return;
+    float s = 0.0f, nz = -1024.0f;
+    if (n < N) { s = scales[g * N + n]; nz = -(1024.0f + static_cast<float>(zps[g * N + n])); }
+    union { _Float16 h[2]; uint32_t u; } pk;
+    pk.h[0] = static_cast<_Float16>(nz);   // exact (integer < 2048)
+    pk.h[1] = static_cast<_Float16>(s);    // RNE
+    sz[g * Npad + n] = pk.u;
+}
+
+__global__ void __launch_bounds__(256) cast_f32_f16_kernel(const float *__restrict__ x, size_t n,
+                                                           __half *__restrict__ y) {
+    const size_t n4 = n / 4;
+    const size_t stride = static_cast<size_t>(gridDim.x) * 256;
+    for (size_t i = blockIdx.x * static_cast<size_t>(256) + threadIdx.x; i < n4; i += stride) {
+        float4 v = reinterpret_cast<const float4 *>(x)[i];
+        union { __half h[4]; uint2 u; } pk;
+        pk.h[0] = __float2half_rn(v.x); pk.h[1] = __float2half_rn(v.y);
+        pk.h[2] = __float2half_rn(v.z); pk.h[3] = __float2half_rn(v.w);
+        reinterpret_cast<uint2 *>(y)[i] = pk.u;
+    }
+    for (size_t i = n4 * 4 + blockIdx.x * static_cast<size_t>(256) + threadIdx.x; i < n; i += stride)
+        y[i] = __float2half_rn(x[i]);
+}
+
+// ---------------------------------------------------------------------------------------------
+// GEMM: Y[M][N] = X[M][K] (f16) . W^[K][N] + b, computed as Y^T = W^^T X^T so that the
+// accumulator's lane index is the token m and 4 consecutive registers hold 4 consecutive
+// output columns n (one 8/16-byte store each).
+//   block tile 256 (m) x 128 (n), 4 waves as 2 (m) x 2 (n), wave tile 128 x 64:
+//   acc[2 n-reps][4 m-reps] of 32x32 f32 = 128 VGPRs.
+//   X tile [256][64] f16 in LDS (2 buffers, 64 KiB), filled by global_load_lds 16 B/lane with
+//   the 16-B chunk index XOR-swizzled by (row>>1)&7 (conflict-free ds_read_b128 fragments).
+//   W fragments stream straight to VGPRs (one coalesced dwordx4 per lane per slab for int4)
+//   one slab ahead, and are dequantized in registers (4 VALU per 2 weights).
+// ---------------------------------------------------------------------------------------------
+template <int BITS>
+struct WSlab { uint32_t w[2][BITS]; };
+
+template <int BITS>
+__device__ __forceinline__ void load_wslab(WSlab<BITS> &ws, const uint32_t *__restrict__ wdev, size_t nk,
+                                           size_t nt0, size_t kt, int lane) {
+#pragma unroll
+    for (int rep = 0; rep < 2; ++rep) {
+        const uint32_t *p = wdev + (((nt0 + rep) * nk + kt) * 64 + lane) * BITS;
+        if constexpr (BITS == 4) {
+            uint4 v = *reinterpret_cast<const uint4 *>(p);
+            ws.w[rep][0] = v.x; ws.w[rep][1] = v.y; ws.w[rep][2] = v.z; ws.w[rep][3] = v.w;
+        } else if constexpr (BITS == 2) {
+            uint2 v = *reinterpret_cast<const uint2 *>(p);
+            ws.w[rep][0] = v.x; ws.w[rep][1] = v.y;
+        } else {
+            uint4 a = *reinterpret_cast<const uint4 *>(p), b = *reinterpret_cast<const uint4 *>(p + 4);
+            ws.w[rep][0] = a.x; ws.w[rep][1] = a.y; ws.w[rep][2] = a.z; ws.w[rep][3] = a.w;
+            ws.w[rep][4] = b.x; ws.w[rep][5] = b.y; ws.w[rep][6] = b.z; ws.w[rep][7] = b.w;
+        }
+    }
+}
+
+// Dequantizes the A fragment (8 f16) of substep s from the slab words.
+template <int BITS>
+__device__ __forceinline__ half8_t dequant_frag(const uint32_t (&w)[BITS], int s, half2_t nz, half2_t sc) {
+    constexpr int PPW = 16 / BITS;
+    constexpr uint32_t mask2 = ((1u << BITS) - 1u) * 0x00010001u;
+    half8_t r;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        const int P = s * 4 + v;
+        const uint32_t word = w[P / PPW];
+        const uint32_t t = ((word >> (BITS * (P % PPW))) & mask2) | 0x64006400u;
+        half2_t h = __builtin_bit_cast(half2_t, t);
+        h = h + nz;        // exact: q - zp
+        h = h * sc;        // one f16 rounding of (q - zp) * scale
+        r[2 * v] = h[0];
+        r[2 * v + 1] = h[1];
+    }
+    return r;
+}
+
+__device__ __forceinline__ void glds16(const void *gsrc, void *ldst) {
+    __builtin_amdgcn_global_load_lds((gbl_void_ptr)(const_cast<void *>(gsrc)), (lds_void_ptr)(ldst), 16, 0, 0);
+}
+
+template <typename YT>
+__device__ __forceinline__ void store4(YT *p, float a, float b, float c, float d);
+template <>
+__device__ __forceinline__ void store4<float>(float *p, float a, float b, float c, float d) {
+    *reinterpret_cast<float4 *>(p) = make_float4(a, b, c, d);
+}
+template <>
+__device__ __forceinline__ void store4<__half>(__half *p, float a, float b, float c, float d) {
+    union { __half h[4]; uint2 u; } pk;
+    pk.h[0] = __float2half_rn(a); pk.h[1] = __float2half_rn(b);
+    pk.h[2] = __float2half_rn(c); pk.h[3] = __float2half_rn(d);
+    *reinterpret_cast<uint2 *>(p) = pk.u;
+}
+template <typename YT>
+__device__ __forceinline__ void store1(YT *p, float a);
+template <>
+__device__ __forceinline__ void store1<float>(float *p, float a) { *p = a; }
+template <>
+__device__ __forceinline__ void store1<__half>(__half *p, float a) { *p = __float2half_rn(a); }
+
+template <int BITS, typename YT>
+__global__ void __launch_bounds__(kThreads, 2)
+wq_gemm_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdev,
+               const uint32_t *__restrict__ sz, const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad,
+               int group, int nbm, int nbn) {
+    __shared__ __attribute__((aligned(16))) _Float16 xs[2 * kBM * kBK];   // the ONE LDS array
+
+    // XCD-aware bijective remap: consecutive logical tiles (same bm row panel of X) share an XCD.
+    const int nb = nbm * nbn, orig = blockIdx.x;
+    const int xcd = orig % kXCDs, q8 = nb / kXCDs, r8 = nb % kXCDs;
+    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / kXCDs;
+    const int bm = wgid / nbn, bn = wgid % nbn;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int m0 = bm * kBM, n0 = bn * kBN;
+    const size_t nk = static_cast<size_t>(K) / kBK;
+    const size_t nt0 = static_cast<size_t>(n0 + wn * 64) >> 5;
+
+    // glds source rows for this thread (8 instructions x 32 rows per buffer).
+    const int chunk_st = lane & 7;
+    const __half *xsrc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int row = i * 32 + wave * 8 + (lane >> 3);
+        int grow = m0 + row;
+        grow = grow < M ? grow : M - 1;
+        const int c = chunk_st ^ ((row >> 1) & 7);
+        xsrc[i] = X + static_cast<size_t>(grow) * K + c * 8;
+    }
+    auto stage_x = [&](int buf, size_t kt) {
+        _Float16 *base = xs + buf * (kBM * kBK) + wave * 512;   // 1 KiB per wave-instruction
+#pragma unroll
+        for (int i = 0; i < 8; ++i) glds16(xsrc[i] + kt * kBK, base + i * 2048);
+    };
+
+    float16_t acc[2][4];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
+
+    auto load_sz = [&](size_t kt, uint32_t (&out)[2]) {
+        const size_t g = (kt * kBK) / group;
+#pragma unroll
+        for (int rep = 0; rep < 2; ++rep) out[rep] = sz[g * Npad + n0 + wn * 64 + rep * 32 + (lane & 31)];
+    };
+
+    WSlab<BITS> wcur, wnxt;
+    uint32_t szc[2], szn[2];
+    stage_x(0, 0);
+    load_wslab<BITS>(wcur, wdev, nk, nt0, 0, lane);
+    load_sz(0, szc);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    // LDS fragment read offsets (in halves) for the 4 m-reps; chunk = 2*s + (lane>>5).
+    int rowoff[4], rowx[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int row = wm * 128 + r * 32 + (lane & 31);
+        rowoff[r] = row * kBK;
+        rowx[r] = (row >> 1) & 7;
+    }
+    const int hsel = lane >> 5;
+
+    for (size_t kt = 0; kt < nk; ++kt) {
+        const int cur = static_cast<int>(kt & 1);
+        if (kt + 1 < nk) {
+            stage_x(cur ^ 1, kt + 1);
+            load_wslab<BITS>(wnxt, wdev, nk, nt0, kt + 1, lane);
+            load_sz(kt + 1, szn);
+        }
+        half2_t nz[2], sc[2];
+#pragma unroll
+        for (int rep = 0; rep < 2; ++rep) {
+            half2_t p = __builtin_bit_cast(half2_t, szc[rep]);
+            nz[rep] = half2_t{p[0], p[0]};
+            sc[rep] = half2_t{p[1], p[1]};
+        }
+        const _Float16 *xb = xs + cur * (kBM * kBK);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            half8_t a0 = dequant_frag<BITS>(wcur.w[0], s, nz[0], sc[0]);
+            half8_t a1 = dequant_frag<BITS>(wcur.w[1], s, nz[1], sc[1]);
+            const int chunk = 2 * s + hsel;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const half8_t b = *reinterpret_cast<const half8_t *>(xb + rowoff[r] + ((chunk ^ rowx[r]) << 3));
+                acc[0][r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b, acc[0][r], 0, 0, 0);
+                acc[1][r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b, acc[1][r], 0, 0, 0);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (kt + 1 < nk) {
+            wcur = wnxt;
+            szc[0] = szn[0]; szc[1] = szn[1];
+        }
+    }
+
+    // Epilogue: acc[rep][r] reg e -> n = nbase + (e&3) + 8*(e>>2) + 4*(lane>>5), m = mbase + (lane&31).
+    const bool vec_ok = (N % 4) == 0;
+#pragma unroll
+    for (int rep = 0; rep < 2; ++rep) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = m0 + wm * 128 + r * 32 + (lane & 31);
+            if (m >= M) continue;
+            YT *yrow = Y + static_cast<size_t>(m) * N;
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd) {
+                const int n = n0 + wn * 64 + rep * 32 + 8 * qd + 4 * hsel;
+                if (n >= N) continue;
+                const float4 bv = *reinterpret_cast<const float4 *>(bias + n);
+                const float y0 = acc[rep][r][4 * qd + 0] + bv.x, y1 = acc[rep][r][4 * qd + 1] + bv.y;
+                const float y2 = acc[rep][r][4 * qd + 2] + bv.z, y3 = acc[rep][r][4 * qd + 3] + bv.w;
+                if (vec_ok) {
+                    store4<YT>(yrow + n, y0, y1, y2, y3);
+                } else {
+                    store1<YT>(yrow + n, y0);
+                    if (n + 1 < N) store1<YT>(yrow + n + 1, y1);
+                    if (n + 2 < N) store1<YT>(yrow + n + 2, y2);
+                    if (n + 3 < N) store1<YT>(yrow + n + 3, y3);
+                }
+            }
+        }
+    }
+}
+
+template <int BITS>
+int launch_gemm(const dllm_linear *h, const __half *X, size_t M, void *Y, int y_dtype, hipStream_t st) {
+    const int nbm = static_cast<int>((M + kBM - 1) / kBM), nbn = static_cast<int>(h->Npad / kBN);
+    const unsigned nb = static_cast<unsigned>(nbm) * nbn;
+    if (y_dtype == DLLM_F32)
+        wq_gemm_kernel<BITS, float><<<nb, kThreads, 0, st>>>(X, (int)M, (int)h->K, h->wdev, h->sz, h->bias,
+                                                             static_cast<float *>(Y), (int)h->N, (int)h->Npad,
+                                                             (int)h->group, nbm, nbn);
+    else
+        wq_gemm_kernel<BITS, __half><<<nb, kThreads, 0, st>>>(X, (int)M, (int)h->K, h->wdev, h->sz, h->bias,
+                                                              static_cast<__half *>(Y), (int)h->N, (int)h->Npad,
+                                                              (int)h->group, nbm, nbn);
+    DLLM_LAUNCH_CHECK();
+    return DLLM_OK;
+}
+
+void free_linear(dllm_linear *h) {
+    if (!h) return;
+    (void)hipFree(h->wdev); (void)hipFree(h->sz); (void)hipFree(h->canon); (void)hipFree(h->scales);
+    (void)hipFree(h->zps); (void)hipFree(h->bias); (void)hipFree(h->xws);
+    delete h;
+}
+
+int check_shape(size_t K, size_t N, uint8_t bits, size_t group) {
+    if (bits != 2 && bits != 4 && bits != 8)
+        return fail(DLLM_ERR_UNSUPPORTED, "linear layer supports bits in {2, 4, 8}");
+    if (K == 0 || N == 0) return fail(DLLM_ERR_SHAPE_MISMATCH, "K and N must be >= 1");
+    if (K % kBK) return fail(DLLM_ERR_SHAPE_MISMATCH, "K must be a multiple of 64");
+    if (group == 0 || group % kBK) return fail(DLLM_ERR_INVALID_PARAMS, "group must be a positive multiple of 64");
+    if (K > (1u << 30) || N > (1u << 30)) return fail(DLLM_ERR_SHAPE_MISMATCH, "dimension too large");
+    return DLLM_OK;
+}
+
+int alloc_linear(size_t K, size_t N, uint8_t bits, size_t group, dllm_linear **out) {
+    dllm_linear *h = new (std::nothrow) dllm_linear();
+    if (!h) return fail(DLLM_ERR_HIP, "out of host memory");
+    h->K = K; h->N = N; h->bits = bits; h->group = group;
+    h->Npad = (N + kBN - 1) / kBN * kBN;
+    h->G = (K + group - 1) / group;
+    (void)hipGetDevice(&h->device);
+    auto A = [&](void **p, size_t bytes) { return hipMalloc(p, std::max<size_t>(bytes, 16)); };
+    hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->wdev), h->Npad * K * bits / 8);
+    if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->sz), h->G * h->Npad * 4);
+    if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->canon), canon_words(K, N, bits) * 4);
+    if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->scales), h->G * N * 4);
+    if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->zps), h->G * N);
+    if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->bias), h->Npad * 4);
+    if (e != hipSuccess) {
+        free_linear(h);
+        return fail(DLLM_ERR_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
+    }
+    *out = h;
+    return DLLM_OK;
+}
+
+int finish_linear(dllm_linear *h, const float *bias, hipStream_t st) {
+    DLLM_HIP_TRY(hipMemsetAsync(h->bias, 0, h->Npad * 4, st));
+    if (bias) DLLM_HIP_TRY(hipMemcpyAsync(h->bias, bias, h->N * 4, hipMemcpyDeviceToDevice, st));
+    dim3 gf(static_cast<unsigned>((h->Npad + 255) / 256), static_cast<unsigned>(h->K / 64));
+    build_fragments_kernel<<<gf, 256, 0, st>>>(h->canon, h->K, h->N, h->Npad, h->bits, h->wdev);
+    DLLM_LAUNCH_CHECK();
+    dim3 gs(static_cast<unsigned>((h->Npad + 255) / 256), static_cast<unsigned>(h->G));
+    build_sz_kernel<<<gs, 256, 0, st>>>(h->scales, h->zps, h->G, h->N, h->Npad, h->sz);
+    DLLM_LAUNCH_CHECK();
+    return DLLM_OK;
+}
+
+}  // namespace
+}  // namespace dllm
+
+using namespace dllm;
+
+extern "C" {
+
+int dllm_linear_create(const float *W, const float *bias, size_t K, size_t N, uint8_t bits, size_t group,
+                       dllm_linear_t *out, dllm_stream_t stream) {
+    if (!out || !W) return fail(DLLM_ERR_INVALID_PARAMS, "null pointer");
+    int rc = check_shape(K, N, bits, group);
+    if (rc) return rc;
+    dllm_linear *h = nullptr;
+    if ((rc = alloc_linear(K, N, bits, group, &h))) return rc;
+    hipStream_t st = as_stream(stream);
+    hipError_t e = hipMemsetAsync(h->canon, 0, canon_words(K, N, bits) * 4, st);
+    if (e != hipSuccess) { free_linear(h); return fail(DLLM_ERR_HIP, hipGetErrorString(e)); }
+    dim3 g(static_cast<unsigned>((N + 255) / 256), static_cast<unsigned>(h->G));
+    quantize_weights_kernel<<<g, 256, 0, st>>>(W, K, N, bits, static_cast<int>(group), h->canon, h->scales, h->zps);
+    if (hipGetLastError() != hipSuccess) { free_linear(h); return fail(DLLM_ERR_HIP, "quantize_weights launch"); }
+    if ((rc = finish_linear(h, bias, st))) { free_linear(h); return rc; }
+    *out = h;
+    return DLLM_OK;
+}
+
+int dllm_linear_create_quantized(const uint8_t *packed_codes, const float *scales, const uint8_t *zps,
+                                 const float *bias, size_t K, size_t N, uint8_t bits, size_t group,
+                                 dllm_linear_t *out, dllm_stream_t stream) {
+    if (!out || !packed_codes || !scales || !zps) return fail(DLLM_ERR_INVALID_PARAMS, "null pointer");
+    int rc = check_shape(K, N, bits, group);
+    if (rc) return rc;
+    dllm_linear *h = nullptr;
+    if ((rc = alloc_linear(K, N, bits, group, &h))) return rc;
+    hipStream_t st = as_stream(stream);
+    const size_t nbytes = (K * N * bits + 7) / 8;
+    hipError_t e = hipMemsetAsync(h->canon, 0, canon_words(K, N, bits) * 4, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(h->canon, packed_codes, nbytes, hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(h->scales, scales, h->G * N * 4, hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(h->zps, zps, h->G * N, hipMemcpyDeviceToDevice, st);
+    if (e != hipSuccess) { free_linear(h); return fail(DLLM_ERR_HIP, hipGetErrorString(e)); }
+    if ((rc = finish_linear(h, bias, st))) { free_linear(h); return rc; }
+    *out = h;
+    return DLLM_OK;
+}
+
+int dllm_linear_forward(dllm_linear_t h, const void *X, size_t M, int x_dtype, void *Y, int y_dtype,
+                        dllm_stream_t stream) {
+    if (!h) return fail(DLLM_ERR_INVALID_PARAMS, "null handle");
+    if ((x_dtype != DLLM_F32 && x_dtype != DLLM_F16) || (y_dtype != DLLM_F32 && y_dtype != DLLM_F16))
+        return fail(DLLM_ERR_UNSUPPORTED, "dtype must be DLLM_F32 or DLLM_F16");
+    if (M == 0) return DLLM_OK;
+    if (!X || !Y) return fail(DLLM_ERR_INVALID_PARAMS, "null pointer");
+    if (M > (1u << 30)) return fail(DLLM_ERR_SHAPE_MISMATCH, "M too large");
+    if ((reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(Y) & 15))
+        return fail(DLLM_ERR_INVALID_PARAMS, "X and Y must be 16-byte aligned");
+    hipStream_t st = as_stream(stream);
+    const __half *Xh = static_cast<const __half *>(X);
+    if (x_dtype == DLLM_F32) {
+        std::lock_guard<std::mutex> lk(h->mu);
+        const size_t need = M * h->K;
+        if (h->xws_elems < need) {
+            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+            (void)hipStreamIsCapturing(st, &cs);
+            if (cs != hipStreamCaptureStatusNone)
+                return fail(DLLM_ERR_INVALID_PARAMS, "f32 X workspace must be grown before stream capture");
+            DLLM_HIP_TRY(hipStreamSynchronize(st));
+            (void)hipFree(h->xws);
+            h->xws = nullptr;
+            h->xws_elems = 0;
+            DLLM_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&h->xws), need * sizeof(__half)));
+            h->xws_elems = need;
+        }
+        cast_f32_f16_kernel<<<grid_for(need / 4 + 1, 256, kCUs * 8), 256, 0, st>>>(static_cast<const float *>(X),
+                                                                                     need, h->xws);
+        DLLM_LAUNCH_CHECK();
+        Xh = h->xws;
+    }
+    switch (h->bits) {
+    case 2: return launch_gemm<2>(h, Xh, M, Y, y_dtype, st);
+    case 4: return launch_gemm<4>(h, Xh, M, Y, y_dtype, st);
+    case 8: return launch_gemm<8>(h, Xh, M, Y, y_dtype, st);
+    default: return fail(DLLM_ERR_UNSUPPORTED, "bits");
+    }
+}
+
+int dllm_linear_export(dllm_linear_t h, uint8_t *packed_codes, float *scales, uint8_t *zps, dllm_stream_t stream) {
+    if (!h) return fail(DLLM_ERR_INVALID_PARAMS, "null handle");
+    hipStream_t st = as_stream(stream);
+    if (packed_codes)
+        DLLM_HIP_TRY(hipMemcpyAsync(packed_codes, h->canon, (h->K * h->N * h->bits + 7) / 8,
+                                    hipMemcpyDeviceToDevice, st));
+    if (scales) DLLM_HIP_TRY(hipMemcpyAsync(scales, h->scales, h->G * h->N * 4, hipMemcpyDeviceToDevice, st));
+    if (zps) DLLM_HIP_TRY(hipMemcpyAsync(zps, h->zps, h->G * h->N, hipMemcpyDeviceToDevice, st));
+    return DLLM_OK;
+}
+
+int dllm_linear_info(dllm_linear_t h, size_t *K, size_t *N, uint8_t *bits, size_t *group) {
+    if (!h) return fail(DLLM_ERR_INVALID_PARAMS, "null handle");
+    if (K) *K = h->K;
+    if (N) *N = h->N;
+    if (bits) *bits = static_cast<uint8_t>(h->bits);
+    if (group) *group = h->group;
+    return DLLM_OK;
+}
+
+size_t dllm_linear_weight_bytes(dllm_linear_t h) {
+    if (!h) return 0;
+    return h->Npad * h->K * h->bits / 8 + h->G * h->Npad * 4;
+}
+
+int dllm_linear_destroy(dllm_linear_t h) {
+    free_linear(h);
+    return DLLM_OK;
+}
+
+}  // extern "C"

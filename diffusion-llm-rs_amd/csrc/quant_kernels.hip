@@ -1,0 +1,720 @@
+// quant_kernels.hip -- HBM-bound quantize / dequantize / pack kernels for gfx950 (MI355X).
+//
+// Every kernel is a bit-exact restatement of a reference Rust loop (cited per kernel), built with
+// -ffp-contract=off so that no separately rounded Rust f32 op pair is fused into an FMA.
+// Layout: elements are processed in "octets" of 8 consecutive values: 8 codes of b bits are
+// exactly b bytes of the LSB-first packed bitstream (include/dllm_quant.h), so a thread owns
+// whole bytes and no two threads ever touch the same output byte.
+#include "common.hpp"
+
+#include <algorithm>
+#include <cstring>
+
+namespace dllm {
+namespace {
+
+constexpr int kBlock = 256;
+
+// ---------------------------------------------------------------------------------------------
+// Octet load / store helpers
+// ---------------------------------------------------------------------------------------------
+struct F8 { float v[8]; };
+
+// Loads the 8 floats of octet `o` (cnt = number of valid elements, <= 8).  vec: x is 16-B aligned.
+__device__ __forceinline__ F8 load_octet(const float *__restrict__ x, size_t o, int cnt, bool vec) {
+    F8 r;
+    const float *p = x + o * 8;
+    if (vec && cnt == 8) {
+        float4 a = *reinterpret_cast<const float4 *>(p);
+        float4 b = *reinterpret_cast<const float4 *>(p + 4);
+        r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
+        r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r.v[i] = (i < cnt) ? p[i] : 0.0f;
+    }
+    return r;
+}
+
+// Packs 8 codes (each < 2^bits) into the low 8*bits bits of a u64, LSB-first.
+__device__ __forceinline__ uint64_t pack_octet(const uint32_t (&c)[8], int bits) {
+    uint64_t w = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w |= static_cast<uint64_t>(c[i]) << (i * bits);
+    return w;
+}
+
+// Writes the octet's codes: packed -> `bits` bytes (fewer for a partial tail octet),
+// unpacked -> one byte per code.
+__device__ __forceinline__ void store_codes(uint8_t *__restrict__ out, size_t o, int cnt, const uint32_t (&c)[8],
+                                            int bits, bool packed, bool vec) {
+    if (packed) {
+        uint64_t w = pack_octet(c, bits);
+        uint8_t *p = out + o * bits;
+        if (cnt == 8 && vec) {
+            switch (bits) {
+            case 1: *p = static_cast<uint8_t>(w); return;
+            case 2: *reinterpret_cast<uint16_t *>(p) = static_cast<uint16_t>(w); return;
+            case 4: *reinterpret_cast<uint32_t *>(p) = static_cast<uint32_t>(w); return;
+            case 8: *reinterpret_cast<uint64_t *>(p) = w; return;
+            default: break;
+            }
+        }
+        int nbytes = (cnt * bits + 7) / 8;
+        for (int i = 0; i < nbytes; ++i) p[i] = static_cast<uint8_t>(w >> (8 * i));
+    } else {
+        uint8_t *p = out + o * 8;
+        if (cnt == 8 && vec) {
+            uint64_t w = 0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) w |= static_cast<uint64_t>(c[i]) << (8 * i);
+            *reinterpret_cast<uint64_t *>(p) = w;
+        } else {
+            for (int i = 0; i < cnt; ++i) p[i] = static_cast<uint8_t>(c[i]);
+        }
+    }
+}
+
+// Reads the octet's codes back (inverse of store_codes).
+__device__ __forceinline__ void load_codes(const uint8_t *__restrict__ q, size_t o, int cnt, int bits, bool packed,
+                                           bool vec, uint32_t (&c)[8]) {
+    uint64_t w = 0;
+    if (packed) {
+        const uint8_t *p = q + o * bits;
+        if (cnt == 8 && vec && (bits == 1 || bits == 2 || bits == 4 || bits == 8)) {
+            switch (bits) {
+            case 1: w = *p; break;
+            case 2: w = *reinterpret_cast<const uint16_t *>(p); break;
+            case 4: w = *reinterpret_cast<const uint32_t *>(p); break;
+            default: w = *reinterpret_cast<const uint64_t *>(p); break;
+            }
+        } else {
+            int nbytes = (cnt * bits + 7) / 8;
+            for (int i = 0; i < nbytes; ++i) w |= static_cast<uint64_t>(p[i]) << (8 * i);
+        }
+        const uint32_t mask = (1u << bits) - 1u;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) c[i] = static_cast<uint32_t>(w >> (i * bits)) & mask;
+    } else {
+        const uint8_t *p = q + o * 8;
+        if (cnt == 8 && vec) {
+            w = *reinterpret_cast<const uint64_t *>(p);
+        } else {
+            for (int i = 0; i < cnt; ++i) w |= static_cast<uint64_t>(p[i]) << (8 * i);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) c[i] = static_cast<uint32_t>(w >> (8 * i)) & 0xFFu;
+    }
+}
+
+__device__ __forceinline__ void store_f8(void *__restrict__ out, int dtype, size_t o, int cnt, const float (&y)[8],
+                                         bool vec) {
+    if (dtype == DLLM_F32) {
+        float *p = static_cast<float *>(out) + o * 8;
+        if (cnt == 8 && vec) {
+            *reinterpret_cast<float4 *>(p) = make_float4(y[0], y[1], y[2], y[3]);
+            *reinterpret_cast<float4 *>(p + 4) = make_float4(y[4], y[5], y[6], y[7]);
+        } else {
+            for (int i = 0; i < cnt; ++i) p[i] = y[i];
+        }
+    } else {
+        __half *p = static_cast<__half *>(out) + o * 8;
+        if (cnt == 8 && vec) {
+            union { __half h[8]; uint4 u; } pk;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) pk.h[i] = __float2half_rn(y[i]);
+            *reinterpret_cast<uint4 *>(p) = pk.u;
+        } else {
+            for (int i = 0; i < cnt; ++i) p[i] = __float2half_rn(y[i]);
+        }
+    }
+}
+
+__device__ __forceinline__ int octet_count(size_t o, size_t n) {
+    size_t rem = n - o * 8;
+    return rem >= 8 ? 8 : static_cast<int>(rem);
+}
+
+// ---------------------------------------------------------------------------------------------
+// K1: global max/min fold (diffuse-llm-rs/src/quantization.rs:41-46).  f32::max / f32::min
+// ignore NaN and are order-independent on the remaining values, so a tree reduction gives the
+// Rust fold's result exactly (the sign of a zero extremum never reaches the outputs).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void block_minmax(float &mx, float &mn, float *smem /* 2*kBlock/64 */) {
+    mx = wave_max(mx);
+    mn = wave_min(mn);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) { smem[w] = mx; smem[kBlock / 64 + w] = mn; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < kBlock / 64; ++i) { mx = fmaxf(mx, smem[i]); mn = fminf(mn, smem[kBlock / 64 + i]); }
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) minmax_partial_kernel(const float *__restrict__ x, size_t n, size_t head,
+                                                                float2 *__restrict__ partials) {
+    __shared__ float smem[2 * kBlock / 64];
+    float mx = -INFINITY, mn = INFINITY;
+    const size_t gid = blockIdx.x * static_cast<size_t>(kBlock) + threadIdx.x;
+    const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+    if (gid < head) { float v = x[gid]; mx = fmaxf(mx, v); mn = fminf(mn, v); }
+    const size_t nv = (n - head) / 4;
+    const float4 *x4 = reinterpret_cast<const float4 *>(x + head);
+    size_t i = gid;
+    // 4 independent float4 loads in flight per thread per trip.
+    for (; i + 3 * stride < nv; i += 4 * stride) {
+        float4 a = x4[i], b = x4[i + stride], c = x4[i + 2 * stride], d = x4[i + 3 * stride];
+        mx = fmaxf(mx, fmaxf(fmaxf(fmaxf(a.x, a.y), fmaxf(a.z, a.w)), fmaxf(fmaxf(b.x, b.y), fmaxf(b.z, b.w))));
+        mx = fmaxf(mx, fmaxf(fmaxf(fmaxf(c.x, c.y), fmaxf(c.z, c.w)), fmaxf(fmaxf(d.x, d.y), fmaxf(d.z, d.w))));
+        mn = fminf(mn, fminf(fminf(fminf(a.x, a.y), fminf(a.z, a.w)), fminf(fminf(b.x, b.y), fminf(b.z, b.w))));
+        mn = fminf(mn, fminf(fminf(fminf(c.x, c.y), fminf(c.z, c.w)), fminf(fminf(d.x, d.y), fminf(d.z, d.w))));
+    }
+    for (; i < nv; i += stride) {
+        float4 a = x4[i];
+        mx = fmaxf(mx, fmaxf(fmaxf(a.x, a.y), fmaxf(a.z, a.w)));
+        mn = fminf(mn, fminf(fminf(a.x, a.y), fminf(a.z, a.w)));
+    }
+    const size_t tail0 = head + nv * 4;
+    if (gid < n - tail0) { float v = x[tail0 + gid]; mx = fmaxf(mx, v); mn = fminf(mn, v); }
+    block_minmax(mx, mn, smem);
+    if (threadIdx.x == 0) partials[blockIdx.x] = make_float2(mx, mn);
+}
+
+// Reduces the partials and computes (scale, zp) exactly as quantization.rs:49-56.
+__global__ void __launch_bounds__(kBlock) quant_params_kernel(const float2 *__restrict__ partials, int np, int bits,
+                                                              float *__restrict__ params) {
+    __shared__ float smem[2 * kBlock / 64];
+    float mx = -INFINITY, mn = INFINITY;
+    for (int i = threadIdx.x; i < np; i += kBlock) { float2 p = partials[i]; mx = fmaxf(mx, p.x); mn = fminf(mn, p.y); }
+    block_minmax(mx, mn, smem);
+    if (threadIdx.x == 0) {
+        const float q_min = 0.0f;
+        const float q_max = static_cast<float>(1u << bits) - 1.0f;     // :50
+        float scale = (mx - mn) / (q_max - q_min);                      // :52
+        if (scale == 0.0f) scale = 1.0f;                                // :53
+        const float zpf = q_min - mn / scale;                           // :55
+        const uint32_t zp = rs_as_u8(roundf(rs_clamp(zpf, q_min, q_max)));  // :56
+        params[0] = scale;
+        params[1] = static_cast<float>(zp);                             // :67
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K2: quantize map (quantization.rs:59-65) fused with packing (a6).
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) quantize_tensor_kernel(const float *__restrict__ x, size_t n, int bits,
+                                                                 int packed, uint8_t *__restrict__ out,
+                                                                 const float *__restrict__ params, int vec_in,
+                                                                 int vec_out) {
+    const float scale = params[0], zp = params[1];
+    const int hi = (1 << bits) - 1;
+    const size_t noct = (n + 7) / 8;
+    for (size_t o = blockIdx.x * static_cast<size_t>(kBlock) + threadIdx.x; o < noct;
+         o += static_cast<size_t>(gridDim.x) * kBlock) {
+        const int cnt = octet_count(o, n);
+        F8 v = load_octet(x, o, cnt, vec_in);
+        uint32_t c[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            float t = v.v[i] / scale;       // IEEE division (separately rounded)
+            t = t + zp;                     // separately rounded add
+            c[i] = (i < cnt) ? rs_round_i32_clamp(t, hi) : 0u;
+        }
+        store_codes(out, o, cnt, c, bits, packed, vec_out);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K3: dequantize (quantization.rs:81-85): y = (q as f32 - zp) * scale.
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) dequantize_kernel(const uint8_t *__restrict__ q, size_t n, int bits,
+                                                            int packed, const float *__restrict__ params, float s_arg,
+                                                            float z_arg, void *__restrict__ out, int dtype, int vec_in,
+                                                            int vec_out) {
+    const float scale = params ? params[0] : s_arg;
+    const float zp = params ? params[1] : z_arg;
+    const size_t noct = (n + 7) / 8;
+    for (size_t o = blockIdx.x * static_cast<size_t>(kBlock) + threadIdx.x; o < noct;
+         o += static_cast<size_t>(gridDim.x) * kBlock) {
+        const int cnt = octet_count(o, n);
+        uint32_t c[8];
+        load_codes(q, o, cnt, bits, packed, vec_in, c);
+        float y[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            float d = static_cast<float>(c[i]) - zp;
+            y[i] = d * scale;
+        }
+        store_f8(out, dtype, o, cnt, y, vec_out);
+    }
+}
+
+// a6 standalone: codes (one per byte) <-> packed bitstream.
+__global__ void __launch_bounds__(kBlock) pack_kernel(const uint8_t *__restrict__ codes, size_t n, int bits,
+                                                      uint8_t *__restrict__ packed, int vec_in, int vec_out) {
+    const size_t noct = (n + 7) / 8;
+    const uint32_t mask = (1u << bits) - 1u;
+    for (size_t o = blockIdx.x * static_cast<size_t>(kBlock) + threadIdx.x; o < noct;
+         o += static_cast<size_t>(gridDim.x) * kBlock) {
+        const int cnt = octet_count(o, n);
+        uint32_t c[8];
+        load_codes(codes, o, cnt, 8, false, vec_in, c);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) c[i] &= mask;
+        store_codes(packed, o, cnt, c, bits, true, vec_out);
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) unpack_kernel(const uint8_t *__restrict__ packed, size_t n, int bits,
+                                                        uint8_t *__restrict__ codes, int vec_in, int vec_out) {
+    const size_t noct = (n + 7) / 8;
+    for (size_t o = blockIdx.x * static_cast<size_t>(kBlock) + threadIdx.x; o < noct;
+         o += static_cast<size_t>(gridDim.x) * kBlock) {
+        const int cnt = octet_count(o, n);
+        uint32_t c[8];
+        load_codes(packed, o, cnt, bits, true, vec_in, c);
+        store_codes(codes, o, cnt, c, 8, false, vec_out);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// a4: DefaultQuantizer (quantization/src/quantize.rs:111-154, :172-184).
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) default_quantize_kernel(const float *__restrict__ x, size_t n, float scale,
+                                                                  float zp, float lo, float hi,
+                                                                  uint8_t *__restrict__ out, int vec_in, int vec_out) {
+    const size_t noct = (n + 7) / 8;
+    for (size_t o = blockIdx.x * static_cast<size_t>(kBlock) + threadIdx.x; o < noct;
+         o += static_cast<size_t>(gridDim.x) * kBlock) {
+        const int cnt = octet_count(o, n);
+        F8 v = load_octet(x, o, cnt, vec_in);
+        uint32_t c[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            float t = v.v[i] / scale;
+            t = t + zp;
+            t = fminf(fmaxf(t, lo), hi);    // .max(min).min(max): NaN -> lo (:119-121)
+            c[i] = rs_as_u8(roundf(t));     // .round(), then `q as u8` (:122, :150)
+        }
+        store_codes(out, o, cnt, c, 8, false, vec_out);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// a8-ii BitQuantizer (prefill-kvquant-rs/lib.rs:39-53) and its row-batched forms.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t bitq(float x, float scale, float zp, float max_val) {
+    float s = (x - zp) / scale;
+    return rs_as_u8(rs_clamp(s, 0.0f, max_val));
+}
+
+__global__ void __launch_bounds__(kBlock) bit_quantize_kernel(const float *__restrict__ x, size_t n, float scale,
+                                                              float zp, float max_val, uint8_t *__restrict__ out,
+                                                              int vec_in, int vec_out) {
+    const size_t noct = (n + 7) / 8;
+    for (size_t o = blockIdx.x * static_cast<size_t>(kBlock) + threadIdx.x; o < noct;
+         o += static_cast<size_t>(gridDim.x) * kBlock) {
+        const int cnt = octet_count(o, n);
+        F8 v = load_octet(x, o, cnt, vec_in);
+        uint32_t c[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) c[i] = bitq(v.v[i], scale, zp, max_val);
+        store_codes(out, o, cnt, c, 8, false, vec_out);
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) bit_dequantize_kernel(const uint8_t *__restrict__ q, size_t n, float scale,
+                                                                float zp, void *__restrict__ out, int dtype, int vec_in,
+                                                                int vec_out) {
+    const size_t noct = (n + 7) / 8;
+    for (size_t o = blockIdx.x * static_cast<size_t>(kBlock) + threadIdx.x; o < noct;
+         o += static_cast<size_t>(gridDim.x) * kBlock) {
+        const int cnt = octet_count(o, n);
+        uint32_t c[8];
+        load_codes(q, o, cnt, 8, false, vec_in, c);
+        float y[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            float p = static_cast<float>(c[i]) * scale;   // lib.rs:50, no FMA
+            y[i] = p + zp;
+        }
+        store_f8(out, dtype, o, cnt, y, vec_out);
+    }
+}
+
+// PrefillKVQuant::quantize_vectors: the per-row (bits, scale) cycle table, passed by value.
+constexpr int kCycleMax = 64;
+struct CycleTable {
+    float scale[kCycleMax];
+    float max_val[kCycleMax];
+};
+
+// One block per (row, chunk); rows r = r0 + j*rstride (j = blockIdx.y).
+__global__ void __launch_bounds__(kBlock) quantize_rows_cycle_kernel(const float *__restrict__ x, size_t rows,
+                                                                     size_t dim, int ncycle, CycleTable tab,
+                                                                     uint8_t *__restrict__ out) {
+    const size_t r = blockIdx.y;
+    if (r >= rows) return;
+    const int slot = static_cast<int>(r % static_cast<size_t>(ncycle));
+    const float scale = tab.scale[slot], max_val = tab.max_val[slot];
+    const float *xr = x + r * dim;
+    uint8_t *orow = out + r * dim;
+    for (size_t i = blockIdx.x * static_cast<size_t>(kBlock) + threadIdx.x; i < dim;
+         i += static_cast<size_t>(gridDim.x) * kBlock)
+        orow[i] = static_cast<uint8_t>(bitq(xr[i], scale, 0.0f, max_val));
+}
+
+// a8-iii compress_vector (diffusion_prefill/src/prefill_kv.rs:104-121): one block per row.
+__global__ void __launch_bounds__(kBlock) compress_rows_kernel(const float *__restrict__ x, size_t dim, float levels,
+                                                               uint8_t *__restrict__ out, float *__restrict__ scales,
+                                                               float *__restrict__ zps) {
+    __shared__ float smem[2 * kBlock / 64];
+    __shared__ float sp[2];
+    const size_t r = blockIdx.x;
+    const float *xr = x + r * dim;
+    float mx = -INFINITY, mn = INFINITY;
+    for (size_t i = threadIdx.x; i < dim; i += kBlock) { float v = xr[i]; mx = fmaxf(mx, v); mn = fminf(mn, v); }
+    block_minmax(mx, mn, smem);
+    if (threadIdx.x == 0) {
+        const float scale = (mx - mn) / levels;   // :107
+        sp[0] = scale; sp[1] = mn;                 // :108 zero_point = min
+        scales[r] = scale; zps[r] = mn;
+    }
+    __syncthreads();
+    const float scale = sp[0], zp = sp[1];
+    uint8_t *orow = out + r * dim;
+    for (size_t i = threadIdx.x; i < dim; i += kBlock) orow[i] = static_cast<uint8_t>(bitq(xr[i], scale, zp, levels));
+}
+
+__global__ void __launch_bounds__(kBlock) decompress_rows_kernel(const uint8_t *__restrict__ q, size_t rows, size_t dim,
+                                                                 const float *__restrict__ scales,
+                                                                 const float *__restrict__ zps,
+                                                                 float *__restrict__ out) {
+    const size_t total = rows * dim;
+    for (size_t i = blockIdx.x * static_cast<size_t>(kBlock) + threadIdx.x; i < total;
+         i += static_cast<size_t>(gridDim.x) * kBlock) {
+        const size_t r = i / dim;
+        float p = static_cast<float>(q[i]) * scales[r];
+        out[i] = p + zps[r];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// a10: CalibrationData::update (quantization/src/calibrate.rs:42-69) on the device.
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) calib_fold_kernel(const float2 *__restrict__ partials, int np,
+                                                            float *__restrict__ stats) {
+    __shared__ float smem[2 * kBlock / 64];
+    float mx = -3.40282347e+38f, mn = 3.40282347e+38f;   // fold seeds (f32::MIN, f32::MAX), :43
+    for (int i = threadIdx.x; i < np; i += kBlock) { float2 p = partials[i]; mx = fmaxf(mx, p.x); mn = fminf(mn, p.y); }
+    block_minmax(mx, mn, smem);
+    if (threadIdx.x == 0) {
+        stats[0] = fminf(stats[0], mn);   // :47
+        stats[1] = fmaxf(stats[1], mx);   // :48
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) calib_hist_kernel(const float *__restrict__ x, size_t n,
+                                                            const float *__restrict__ stats,
+                                                            unsigned long long *__restrict__ hist, int num_bins,
+                                                            int use_lds) {
+    extern __shared__ unsigned int lhist[];
+    const float mn = stats[0], mx = stats[1];
+    if (!(mx > mn)) return;                                   // :59
+    const float bw = (mx - mn) / static_cast<float>(num_bins); // :60
+    if (use_lds) {
+        for (int b = threadIdx.x; b < num_bins; b += kBlock) lhist[b] = 0u;
+        __syncthreads();
+    }
+    for (size_t i = blockIdx.x * static_cast<size_t>(kBlock) + threadIdx.x; i < n;
+         i += static_cast<size_t>(gridDim.x) * kBlock) {
+        const float v = x[i];
+        if (v >= mn && v <= mx) {                             // :62
+            float f = floorf((v - mn) / bw);                  // :63
+            unsigned long long b = (f > 0.0f) ? static_cast<unsigned long long>(f) : 0ull;  // `as usize`
+            if (f >= 18446744073709551616.0f) b = ~0ull;
+            if (b > static_cast<unsigned long long>(num_bins - 1)) b = num_bins - 1;        // :64
+            if (use_lds) atomicAdd(&lhist[b], 1u);
+            else atomicAdd(&hist[b], 1ull);
+        }
+    }
+    if (use_lds) {
+        __syncthreads();
+        for (int b = threadIdx.x; b < num_bins; b += kBlock)
+            if (lhist[b]) atomicAdd(&hist[b], static_cast<unsigned long long>(lhist[b]));
+    }
+}
+
+inline bool aligned(const void *p, size_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; }
+
+inline unsigned octet_grid(size_t n) { return grid_for((n + 7) / 8, kBlock, kCUs * 16); }
+
+constexpr unsigned kMinmaxBlocks = 1024;
+
+inline int launch_minmax(const float *x, size_t n, float2 *partials, unsigned nblk, hipStream_t st) {
+    size_t head = 0;
+    if (aligned(x, 4)) head = ((16 - (reinterpret_cast<uintptr_t>(x) & 15)) & 15) / 4;
+    else return fail(DLLM_ERR_INVALID_PARAMS, "x must be 4-byte aligned");
+    if (head > n) head = n;
+    minmax_partial_kernel<<<nblk, kBlock, 0, st>>>(x, n, head, partials);
+    DLLM_LAUNCH_CHECK();
+    return DLLM_OK;
+}
+
+inline unsigned minmax_blocks(size_t n) { return grid_for((n + 15) / 16, kBlock, kMinmaxBlocks); }
+
+}  // namespace
+}  // namespace dllm
+
+using namespace dllm;
+
+// =============================================================================================
+// C-ABI
+// =============================================================================================
+extern "C" {
+
+size_t dllm_quantize_tensor_workspace(size_t n) { return sizeof(float2) * minmax_blocks(n); }
+
+int dllm_quantize_tensor(const float *x, size_t n, uint8_t bits, int packed, uint8_t *out, float *params_out,
+                         void *workspace, size_t workspace_bytes, dllm_stream_t stream) {
+    if (bits < 1 || bits > 8) return fail(DLLM_ERR_INVALID_PARAMS, "Bits must be between 1 and 8");
+    if (!params_out || (n && (!x || !out))) return fail(DLLM_ERR_INVALID_PARAMS, "null pointer");
+    const unsigned nblk = minmax_blocks(n);
+    if (!workspace || workspace_bytes < sizeof(float2) * nblk)
+        return fail(DLLM_ERR_INVALID_PARAMS, "workspace too small (see dllm_quantize_tensor_workspace)");
+    hipStream_t st = as_stream(stream);
+    float2 *partials = static_cast<float2 *>(workspace);
+    if (n) {
+        int rc = launch_minmax(x, n, partials, nblk, st);
+        if (rc) return rc;
+    }
+    quant_params_kernel<<<1, kBlock, 0, st>>>(partials, n ? static_cast<int>(nblk) : 0, bits, params_out);
+    DLLM_LAUNCH_CHECK();
+    if (n) {
+        quantize_tensor_kernel<<<octet_grid(n), kBlock, 0, st>>>(x, n, bits, packed, out, params_out,
+                                                                 aligned(x, 16), aligned(out, 8));
+        DLLM_LAUNCH_CHECK();
+    }
+    return DLLM_OK;
+}
+
+static int dequant_common(const uint8_t *q, size_t n, uint8_t bits, int packed, const float *params, float s,
+                          float z, void *out, int out_dtype, dllm_stream_t stream) {
+    if (bits < 1 || bits > 8) return fail(DLLM_ERR_INVALID_PARAMS, "Bits must be between 1 and 8");
+    if (out_dtype != DLLM_F32 && out_dtype != DLLM_F16) return fail(DLLM_ERR_UNSUPPORTED, "out_dtype");
+    if (!n) return DLLM_OK;
+    if (!q || !out) return fail(DLLM_ERR_INVALID_PARAMS, "null pointer");
+    dequantize_kernel<<<octet_grid(n), kBlock, 0, as_stream(stream)>>>(q, n, bits, packed, params, s, z, out,
+                                                                       out_dtype, aligned(q, 8), aligned(out, 16));
+    DLLM_LAUNCH_CHECK();
+    return DLLM_OK;
+}
+
+int dllm_dequantize_tensor(const uint8_t *q, size_t n, uint8_t bits, int packed, const float *params, void *out,
+                           int out_dtype, dllm_stream_t stream) {
+    if (!params) return fail(DLLM_ERR_INVALID_PARAMS, "params is null");
+    return dequant_common(q, n, bits, packed, params, 0.f, 0.f, out, out_dtype, stream);
+}
+
+int dllm_dequantize_tensor_scalar(const uint8_t *q, size_t n, uint8_t bits, int packed, float scale, float zp,
+                                  void *out, int out_dtype, dllm_stream_t stream) {
+    return dequant_common(q, n, bits, packed, nullptr, scale, zp, out, out_dtype, stream);
+}
+
+float dllm_compression_ratio(size_t numel, size_t len, uint8_t bits) {
+    const size_t original = numel * 4;                      // quantization.rs:121
+    const size_t compressed = (len * bits + 7) / 8;         // :122
+    return static_cast<float>(original) / static_cast<float>(compressed);
+}
+
+size_t dllm_packed_bytes(size_t n, uint8_t bits) { return (n * bits + 7) / 8; }
+
+int dllm_pack(const uint8_t *codes, size_t n, uint8_t bits, uint8_t *packed, dllm_stream_t stream) {
+    if (bits < 1 || bits > 8) return fail(DLLM_ERR_INVALID_PARAMS, "bits must be in 1..=8");
+    if (!n) return DLLM_OK;
+    pack_kernel<<<octet_grid(n), kBlock, 0, as_stream(stream)>>>(codes, n, bits, packed, aligned(codes, 8),
+                                                                 aligned(packed, 8));
+    DLLM_LAUNCH_CHECK();
+    return DLLM_OK;
+}
+
+int dllm_unpack(const uint8_t *packed, size_t n, uint8_t bits, uint8_t *codes, dllm_stream_t stream) {
+    if (bits < 1 || bits > 8) return fail(DLLM_ERR_INVALID_PARAMS, "bits must be in 1..=8");
+    if (!n) return DLLM_OK;
+    unpack_kernel<<<octet_grid(n), kBlock, 0, as_stream(stream)>>>(packed, n, bits, codes, aligned(packed, 8),
+                                                                   aligned(codes, 8));
+    DLLM_LAUNCH_CHECK();
+    return DLLM_OK;
+}
+
+int dllm_default_quantize(const float *x, size_t n, int qtype, float scale, int32_t zero_point, uint8_t *out,
+                          dllm_stream_t stream) {
+    float lo, hi;
+    switch (qtype) {   // quantize.rs:139-144
+    case DLLM_QT_INT8: lo = -128.f; hi = 127.f; break;
+    case DLLM_QT_INT4: lo = -8.f; hi = 7.f; break;
+    case DLLM_QT_BINARY: lo = 0.f; hi = 1.f; break;
+    case DLLM_QT_FLOAT8: lo = -127.f; hi = 127.f; break;
+    default: return fail(DLLM_ERR_UNSUPPORTED, "unknown QuantizationType");
+    }
+    if (!n) return DLLM_OK;
+    default_quantize_kernel<<<octet_grid(n), kBlock, 0, as_stream(stream)>>>(
+        x, n, scale, static_cast<float>(zero_point), lo, hi, out, aligned(x, 16), aligned(out, 8));
+    DLLM_LAUNCH_CHECK();
+    return DLLM_OK;
+}
+
+int dllm_default_dequantize(const uint8_t *q, size_t n, float scale, int32_t zero_point, float *out,
+                            dllm_stream_t stream) {
+    // quantize.rs:179-181 == quantization.rs:81-85 with zp = zero_point as f32.
+    return dequant_common(q, n, 8, 0, nullptr, scale, static_cast<float>(zero_point), out, DLLM_F32, stream);
+}
+
+int dllm_calib_update(const float *x, size_t n, float *stats, uint64_t *histogram, size_t num_bins, void *workspace,
+                      size_t workspace_bytes, dllm_stream_t stream) {
+    if (!stats) return fail(DLLM_ERR_INVALID_PARAMS, "stats is null");
+    if (!n) return DLLM_OK;
+    const unsigned nblk = minmax_blocks(n);
+    if (!workspace || workspace_bytes < sizeof(float2) * nblk)
+        return fail(DLLM_ERR_INVALID_PARAMS, "workspace too small (see dllm_quantize_tensor_workspace)");
+    hipStream_t st = as_stream(stream);
+    float2 *partials = static_cast<float2 *>(workspace);
+    int rc = launch_minmax(x, n, partials, nblk, st);
+    if (rc) return rc;
+    calib_fold_kernel<<<1, kBlock, 0, st>>>(partials, static_cast<int>(nblk), stats);
+    DLLM_LAUNCH_CHECK();
+    if (num_bins && histogram) {
+        if (num_bins > 0x7fffffff) return fail(DLLM_ERR_INVALID_PARAMS, "num_bins too large");
+        const int use_lds = num_bins <= 16384;
+        calib_hist_kernel<<<grid_for(n, kBlock, kCUs * 4), kBlock, use_lds ? num_bins * 4 : 0, st>>>(
+            x, n, stats, reinterpret_cast<unsigned long long *>(histogram), static_cast<int>(num_bins), use_lds);
+        DLLM_LAUNCH_CHECK();
+    }
+    return DLLM_OK;
+}
+
+int dllm_calib_compute_params(float mn, float mx, size_t total_samples, uint8_t bits, int symmetric, float *scale,
+                              int32_t *zero_point) {
+    // quantization/src/calibrate.rs:72-110 (host scalar arithmetic, IEEE f32, no contraction).
+    if (total_samples == 0) return fail(DLLM_ERR_CALIBRATION_REQUIRED, "Calibration data required");
+    if (bits > 31) return fail(DLLM_ERR_INVALID_PARAMS, "2u32.pow(bits) overflows");
+    volatile float num_levels = static_cast<float>(1u << bits);
+    volatile float range = mx - mn;
+    if (range <= 1.1920929e-07f) { *scale = 1.0f; *zero_point = 0; return DLLM_OK; }
+    auto as_i32 = [](float f) -> int32_t {
+        if (f != f) return 0;
+        if (f >= 2147483648.0f) return INT32_MAX;
+        if (f <= -2147483648.0f) return INT32_MIN;
+        return static_cast<int32_t>(f);
+    };
+    if (symmetric) {
+        volatile float ma = std::max(std::fabs(mx), std::fabs(mn));
+        volatile float t = ma * 2.0f;
+        volatile float s = t / (num_levels - 1.0f);
+        *scale = s;
+        *zero_point = as_i32(num_levels / 2.0f - 1.0f);
+    } else {
+        volatile float s = range / (num_levels - 1.0f);
+        volatile float q = -mn / s;
+        *scale = s;
+        *zero_point = as_i32(std::round(static_cast<float>(q)));
+    }
+    return DLLM_OK;
+}
+
+int dllm_bit_quantize(const float *x, size_t n, uint32_t bits, float scale, float zero_point, uint8_t *out,
+                      dllm_stream_t stream) {
+    if (bits > 30) return fail(DLLM_ERR_INVALID_PARAMS, "(1 << bits) - 1 overflows i32");
+    if (!n) return DLLM_OK;
+    const float max_val = static_cast<float>((1 << bits) - 1);
+    bit_quantize_kernel<<<octet_grid(n), kBlock, 0, as_stream(stream)>>>(x, n, scale, zero_point, max_val, out,
+                                                                         aligned(x, 16), aligned(out, 8));
+    DLLM_LAUNCH_CHECK();
+    return DLLM_OK;
+}
+
+int dllm_bit_dequantize(const uint8_t *q, size_t n, float scale, float zero_point, void *out, int out_dtype,
+                        dllm_stream_t stream) {
+    if (out_dtype != DLLM_F32 && out_dtype != DLLM_F16) return fail(DLLM_ERR_UNSUPPORTED, "out_dtype");
+    if (!n) return DLLM_OK;
+    bit_dequantize_kernel<<<octet_grid(n), kBlock, 0, as_stream(stream)>>>(q, n, scale, zero_point, out, out_dtype,
+                                                                           aligned(q, 8), aligned(out, 16));
+    DLLM_LAUNCH_CHECK();
+    return DLLM_OK;
+}
+
+int dllm_quantize_vectors(const float *x, size_t rows, size_t dim, const uint8_t *cfg_bits, size_t ncfg,
+                          const uint8_t *req_bits, size_t nreq, uint8_t *out, uint8_t *out_bits,
+                          dllm_stream_t stream) {
+    if (nreq == 0 || rows == 0) return DLLM_OK;   // zip(cycle of empty) yields nothing (lib.rs:132)
+    if (!req_bits || (ncfg && !cfg_bits)) return fail(DLLM_ERR_INVALID_PARAMS, "null config");
+    // Validate every row's quantizer index first: the reference panics mid-loop on the first
+    // out-of-bounds quantizers[bits/2] (lib.rs:133); we launch nothing in that case.
+    for (size_t j = 0; j < nreq && j < rows; ++j) {
+        const size_t qi = req_bits[j] / 2;
+        if (qi >= ncfg) return fail(DLLM_ERR_INVALID_PARAMS, "index out of bounds: quantizers[bits / 2]");
+        if (cfg_bits[qi] > 30 || req_bits[j] > 30) return fail(DLLM_ERR_INVALID_PARAMS, "shift overflow");
+    }
+    if (out_bits)
+        for (size_t r = 0; r < rows; ++r) out_bits[r] = req_bits[r % nreq];
+    const size_t ncycle = std::min(nreq, rows);
+    hipStream_t st = as_stream(stream);
+    const unsigned gx = grid_for(dim, kBlock, 64);
+    // Rows are processed in chunks of kCycleMax cycle slots; for nreq <= kCycleMax one launch.
+    if (ncycle <= static_cast<size_t>(kCycleMax)) {
+        CycleTable tab{};
+        for (size_t j = 0; j < ncycle; ++j) {
+            const uint32_t cb = cfg_bits[req_bits[j] / 2];
+            tab.scale[j] = 1.0f / static_cast<float>((1 << cb) - 1);          // lib.rs:106
+            tab.max_val[j] = static_cast<float>((1 << req_bits[j]) - 1);       // lib.rs:41
+        }
+        for (size_t r0 = 0; r0 < rows; r0 += 65535) {
+            const size_t nr = std::min<size_t>(65535, rows - r0);
+            // Cycle position of row r0 + j is (r0 + j) % nreq; r0 is a multiple of 65535, so
+            // rotate the table for this chunk.
+            CycleTable rt{};
+            for (size_t j = 0; j < ncycle; ++j) {
+                const size_t s = (r0 + j) % nreq;
+                rt.scale[j] = tab.scale[s]; rt.max_val[j] = tab.max_val[s];
+            }
+            quantize_rows_cycle_kernel<<<dim3(gx, nr), kBlock, 0, st>>>(x + r0 * dim, nr, dim,
+                                                                      static_cast<int>(ncycle), rt, out + r0 * dim);
+            DLLM_LAUNCH_CHECK();
+        }
+    } else {
+        // Long cycles: one launch per row with that row's quantizer (rare configuration).
+        for (size_t r = 0; r < rows; ++r) {
+            const uint8_t b = req_bits[r % nreq];
+            const uint32_t cb = cfg_bits[b / 2];
+            const float scale = 1.0f / static_cast<float>((1 << cb) - 1);
+            bit_quantize_kernel<<<grid_for((dim + 7) / 8, kBlock, 64), kBlock, 0, st>>>(
+                x + r * dim, dim, scale, 0.0f, static_cast<float>((1 << b) - 1), out + r * dim, aligned(x + r * dim, 16),
+                aligned(out + r * dim, 8));
+            DLLM_LAUNCH_CHECK();
+        }
+    }
+    return DLLM_OK;
+}
+
+int dllm_compress_vectors(const float *x, size_t rows, size_t dim, uint8_t bits, uint8_t *out, float *scales,
+                          float *zps, dllm_stream_t stream) {
+    if (bits > 31) return fail(DLLM_ERR_INVALID_PARAMS, "1u32 << bits overflows");
+    if (!rows) return DLLM_OK;
+    if (rows > 0x7fffffff) return fail(DLLM_ERR_INVALID_PARAMS, "too many rows");
+    const float levels = static_cast<float>((1u << bits) - 1u);
+    compress_rows_kernel<<<static_cast<unsigned>(rows), kBlock, 0, as_stream(stream)>>>(x, dim, levels, out, scales,
+                                                                                        zps);
+    DLLM_LAUNCH_CHECK();
+    return DLLM_OK;
+}
+
+int dllm_decompress_vectors(const uint8_t *q, size_t rows, size_t dim, const float *scales, const float *zps,
+                            float *out, dllm_stream_t stream) {
+    if (!rows || !dim) return DLLM_OK;
+    decompress_rows_kernel<<<grid_for(rows * dim, kBlock, kCUs * 16), kBlock, 0, as_stream(stream)>>>(
+        q, rows, dim, scales, zps, out);
+    DLLM_LAUNCH_CHECK();
+    return DLLM_OK;
+}
+
+}  // extern "C"

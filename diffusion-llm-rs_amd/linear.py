@@ -1,0 +1,101 @@
+"""Group-quantized linear layer: the GPU replacement of ``SimpleDiffusionModel``'s forward
+(diffuse-llm-rs/src/lib.rs:775-836), W [in, out] quantized per (column, 128-row K-group) with
+``quantize_tensor`` and dequantized inside the MFMA GEMM (C-ABI ``dllm_linear_*``)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib
+from ._lib import check
+from .quantization import _dev, _ptr, _stream
+
+
+class QuantLinear:
+    """Owns a ``dllm_linear_t`` handle (device weights uploaded once; immutable; Send + Sync)."""
+
+    def __init__(self, handle, K: int, N: int, bits: int, group: int):
+        self._h = handle
+        self.K, self.N, self.bits, self.group = K, N, bits, group
+
+    @classmethod
+    def from_weight(cls, W: torch.Tensor, bias: torch.Tensor | None = None, bits: int = 4, group: int = 128):
+        """W f32 [K, N] (the reference's ``weights: Array2<f32>`` of shape [input_dim, output_dim])."""
+        W = _dev(W, torch.float32)
+        K, N = W.shape
+        b = None if bias is None else _dev(bias, torch.float32)
+        h = C.c_void_p()
+        check(_lib.load().dllm_linear_create(_ptr(W), _ptr(b), K, N, bits, group, C.byref(h), _stream()))
+        return cls(h, K, N, bits, group)
+
+    @classmethod
+    def from_quantized(cls, packed_codes: torch.Tensor, scales: torch.Tensor, zps: torch.Tensor, K: int, N: int,
+                       bits: int = 4, group: int = 128, bias: torch.Tensor | None = None):
+        h = C.c_void_p()
+        b = None if bias is None else _dev(bias, torch.float32)
+        check(_lib.load().dllm_linear_create_quantized(
+            _ptr(_dev(packed_codes, torch.uint8)), _ptr(_dev(scales, torch.float32)), _ptr(_dev(zps, torch.uint8)),
+            _ptr(b), K, N, bits, group, C.byref(h), _stream()))
+        return cls(h, K, N, bits, group)
+
+    def forward(self, x: torch.Tensor, out: torch.Tensor | None = None, out_dtype=torch.float16) -> torch.Tensor:
+        """``forward(x) = x . W^ + b`` for x [M, K] (f16 or f32) -> [M, N]."""
+        if x.dim() != 2 or x.shape[1] != self.K:
+            raise _lib.ShapeMismatch(f"x must be [M, {self.K}], got {tuple(x.shape)}")
+        if not x.is_cuda or not x.is_contiguous():
+            x = _dev(x)
+        if x.dtype not in (torch.float16, torch.float32):
+            x = x.to(torch.float16)
+        M = x.shape[0]
+        if out is None:
+            out = torch.empty(M, self.N, dtype=out_dtype, device=x.device)
+        xdt = _lib.F16 if x.dtype == torch.float16 else _lib.F32
+        ydt = _lib.F16 if out.dtype == torch.float16 else _lib.F32
+        check(_lib.load().dllm_linear_forward(self._h, _ptr(x), M, xdt, _ptr(out), ydt, _stream()))
+        return out
+
+    __call__ = forward
+
+    def export(self):
+        """-> (packed codes of the [K][N] code matrix, scales [G][N] f32, zero points [G][N] u8)."""
+        G = (self.K + self.group - 1) // self.group
+        dev = torch.device("cuda")
+        codes = torch.empty((self.K * self.N * self.bits + 7) // 8, dtype=torch.uint8, device=dev)
+        scales = torch.empty(G, self.N, dtype=torch.float32, device=dev)
+        zps = torch.empty(G, self.N, dtype=torch.uint8, device=dev)
+        check(_lib.load().dllm_linear_export(self._h, _ptr(codes), _ptr(scales), _ptr(zps), _stream()))
+        return codes, scales, zps
+
+    def weight_bytes(self) -> int:
+        return int(_lib.load().dllm_linear_weight_bytes(self._h))
+
+    def close(self):
+        if self._h is not None and self._h.value:
+            torch.cuda.current_stream().synchronize()
+            _lib.load().dllm_linear_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class MixedPrecisionStack:
+    """Config 3: L linear layers, layer l quantized at ``bits[l % len(bits)]`` (the reference's
+    ``bits.iter().cycle()`` idiom, prefill-kvquant-rs/lib.rs:132); X_{l+1} = Y_l."""
+
+    def __init__(self, weights, biases=None, bits=(2, 4), group: int = 128):
+        self.layers = []
+        for i, W in enumerate(weights):
+            b = None if biases is None else biases[i]
+            self.layers.append(QuantLinear.from_weight(W, b, bits[i % len(bits)], group))
+
+    def forward(self, x: torch.Tensor, out_dtype=torch.float16) -> torch.Tensor:
+        for i, layer in enumerate(self.layers):
+            x = layer(x, out_dtype=out_dtype if i == len(self.layers) - 1 else torch.float16)
+        return x
+
+    __call__ = forward

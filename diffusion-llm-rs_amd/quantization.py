@@ -1,0 +1,183 @@
+"""Mirror of ``diffuse_llm_rs::quantization`` (diffuse-llm-rs/src/quantization.rs) on the GPU.
+
+Same names, argument meaning and error behaviour as the Rust module; data lives in HBM as torch
+tensors and every computation is a HIP kernel behind the C-ABI (include/dllm_quant.h).
+Differences forced by the device boundary are documented per item (e.g. scale/zero_point stay
+on the device as a 2-float tensor until read, so nothing synchronises the stream).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _dev(t: torch.Tensor, dtype=None) -> torch.Tensor:
+    if not isinstance(t, torch.Tensor):
+        t = torch.as_tensor(np.asarray(t))
+    if dtype is not None and t.dtype != dtype:
+        t = t.to(dtype)
+    if not t.is_cuda:
+        t = t.cuda()
+    return t.contiguous()
+
+
+def packed_bytes(n: int, bits: int) -> int:
+    return (n * bits + 7) // 8
+
+
+def quantize_tensor(data: torch.Tensor, bits: int, packed: bool = False):
+    """quantization.rs:38-68 ``quantize_tensor(data, bits) -> (Vec<u8>, f32, f32)``.
+
+    Returns ``(codes, params)``: codes u8 (one per element, or the packed bitstream when
+    ``packed``), params = device f32[2] {scale, zero_point}.  ``bits`` outside 1..=8 raises
+    InvalidParams (the reference's ``assert!``, :39).
+    """
+    if not 1 <= int(bits) <= 8:
+        raise _lib.InvalidParams("Bits must be between 1 and 8")
+    x = _dev(data, torch.float32).reshape(-1)
+    n = x.numel()
+    out = torch.empty(packed_bytes(n, bits) if packed else n, dtype=torch.uint8, device=x.device)
+    params = torch.empty(2, dtype=torch.float32, device=x.device)
+    L = _lib.load()
+    ws_bytes = L.dllm_quantize_tensor_workspace(n)
+    ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=x.device)
+    check(L.dllm_quantize_tensor(_ptr(x) if n else None, n, bits, int(packed), _ptr(out) if out.numel() else None,
+                                 _ptr(params), _ptr(ws), ws.numel(), _stream()))
+    return out, params
+
+
+def dequantize_tensor(codes: torch.Tensor, scale, zero_point=None, *, bits: int = 8, packed: bool = False,
+                      n: int | None = None, out_dtype=torch.float32) -> torch.Tensor:
+    """quantization.rs:81-85 ``dequantize_tensor(data, scale, zero_point)``.
+
+    ``scale`` may be the device params tensor returned by :func:`quantize_tensor` (then
+    ``zero_point`` is None) or a host float (the literal Rust signature).
+    """
+    q = _dev(codes, torch.uint8).reshape(-1)
+    if n is None:
+        if packed:
+            raise _lib.InvalidParams("n is required for packed codes")
+        n = q.numel()
+    out = torch.empty(n, dtype=out_dtype, device=q.device)
+    dt = _lib.F32 if out_dtype == torch.float32 else _lib.F16
+    L = _lib.load()
+    if isinstance(scale, torch.Tensor) and zero_point is None:
+        params = _dev(scale, torch.float32)
+        check(L.dllm_dequantize_tensor(_ptr(q), n, bits, int(packed), _ptr(params), _ptr(out), dt, _stream()))
+    else:
+        check(L.dllm_dequantize_tensor_scalar(_ptr(q), n, bits, int(packed), float(scale), float(zero_point),
+                                              _ptr(out), dt, _stream()))
+    return out
+
+
+def pack(codes: torch.Tensor, bits: int) -> torch.Tensor:
+    """LSB-first bitstream packing (build-defined; size contract quantization.rs:122)."""
+    c = _dev(codes, torch.uint8).reshape(-1)
+    out = torch.empty(packed_bytes(c.numel(), bits), dtype=torch.uint8, device=c.device)
+    check(_lib.load().dllm_pack(_ptr(c), c.numel(), bits, _ptr(out), _stream()))
+    return out
+
+
+def unpack(packed_codes: torch.Tensor, n: int, bits: int) -> torch.Tensor:
+    p = _dev(packed_codes, torch.uint8).reshape(-1)
+    out = torch.empty(n, dtype=torch.uint8, device=p.device)
+    check(_lib.load().dllm_unpack(_ptr(p), n, bits, _ptr(out), _stream()))
+    return out
+
+
+def compression_ratio(numel: int, length: int, bits: int) -> float:
+    """quantization.rs:120-124."""
+    return float(_lib.load().dllm_compression_ratio(numel, length, bits))
+
+
+@dataclass
+class QuantizedTensor:
+    """quantization.rs:88-125 ``QuantizedTensor {data, shape, scale, zero_point, bits}``.
+
+    ``data`` holds the codes in the packed bitstream (``packed=True``, the size the reference's
+    accounting assumes) or one code per byte; ``params`` = device {scale, zero_point}.
+    """
+
+    data: torch.Tensor
+    shape: tuple
+    params: torch.Tensor
+    bits: int
+    packed: bool = True
+
+    @classmethod
+    def new(cls, data, shape, scale, zero_point, bits, packed=False):
+        """quantization.rs:104-112 (host scale / zero_point)."""
+        d = _dev(data, torch.uint8)
+        params = torch.tensor([float(scale), float(zero_point)], dtype=torch.float32, device=d.device)
+        return cls(d, tuple(shape), params, int(bits), packed)
+
+    @classmethod
+    def quantize(cls, t: torch.Tensor, bits: int, packed: bool = True):
+        codes, params = quantize_tensor(t, bits, packed=packed)
+        return cls(codes, tuple(t.shape), params, int(bits), packed)
+
+    def numel(self) -> int:
+        return math.prod(self.shape)
+
+    @property
+    def scale(self) -> float:
+        return float(self.params[0].item())
+
+    @property
+    def zero_point(self) -> float:
+        return float(self.params[1].item())
+
+    def dequantize(self, out_dtype=torch.float32) -> torch.Tensor:
+        """quantization.rs:115-117."""
+        return dequantize_tensor(self.data, self.params, bits=self.bits, packed=self.packed, n=self.numel(),
+                                 out_dtype=out_dtype)
+
+    def codes(self) -> torch.Tensor:
+        """One code per byte (the reference's ``data`` field)."""
+        return unpack(self.data, self.numel(), self.bits) if self.packed else self.data
+
+    def compression_ratio(self) -> float:
+        """quantization.rs:120-124: ``(prod(shape) * 4) / ceil(len * bits / 8)``."""
+        return compression_ratio(self.numel(), self.numel(), self.bits)
+
+
+@dataclass
+class QuantizedKVCacheEntry:
+    """quantization.rs:128-176: K and V each quantized per tensor (own scale / zero point)."""
+
+    keys: QuantizedTensor
+    values: QuantizedTensor
+    seq_len: int = field(default=0)
+
+    @classmethod
+    def new(cls, keys: torch.Tensor, values: torch.Tensor, bits: int, packed: bool = True):
+        """quantization.rs:140-157 (keys/values are [num_layers, seq, hidden])."""
+        k = QuantizedTensor.quantize(keys, bits, packed)
+        v = QuantizedTensor.quantize(values, bits, packed)
+        return cls(k, v, int(keys.shape[1]) if keys.dim() > 1 else 0)
+
+    def dequantize_keys(self, out_dtype=torch.float32) -> torch.Tensor:
+        """quantization.rs:160-166."""
+        return self.keys.dequantize(out_dtype).reshape(self.keys.shape)
+
+    def dequantize_values(self, out_dtype=torch.float32) -> torch.Tensor:
+        """quantization.rs:169-175."""
+        return self.values.dequantize(out_dtype).reshape(self.values.shape)
+
+    def memory_usage(self) -> int:
+        """Packed bytes of K and V (the accounting of diffuse-llm-rs/src/lib.rs:279-302)."""
+        return sum(packed_bytes(t.numel(), t.bits) for t in (self.keys, self.values))

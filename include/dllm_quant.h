@@ -1,0 +1,180 @@
+/*
+ * dllm_quant.h -- C-ABI drop-in boundary for diffusion-llm-rs's quantized inference hot path,
+ * implemented by hand-written HIP kernels for MI355X (gfx950) in libdllm_hip.so.
+ *
+ * The reference (zetareticula/diffusion-llm-rs, Rust, CPU-only) has no FFI: its operator surface
+ * is three in-process Rust APIs.  Each entry point below names the Rust
+ * item it replaces (paths relative to the reference root).  Conventions:
+ *   - return int status: 0 = Ok; 1..7 = quantization::QuantizationError discriminant order + 1
+ *     (quantization/src/error.rs:18-40); reference panics (assert!, out-of-bounds index) map to
+ *     DLLM_ERR_INVALID_PARAMS; 16+ = HIP / runtime errors.  dllm_last_error() gives a message.
+ *   - plain pointers and sizes only.  Unless a name ends in _host, every data pointer is DEVICE
+ *     memory and the call is asynchronous on `stream` (a hipStream_t; NULL = default stream);
+ *     nothing is allocated or synchronised inside (graph-capturable).  The *_host variants take
+ *     host pointers, stage through device memory and synchronise (parity/test convenience).
+ *   - quantized codes are either one code per byte ("unpacked", the reference's storage,
+ *     diffuse-llm-rs/src/quantization.rs:59-65) or the packed LSB-first bitstream below.
+ *   - handles (dllm_linear_t) own device memory, are immutable after create and may be used
+ *     from several threads on distinct streams (the reference's Send + Sync model bound).
+ *
+ * Packed layout (build-defined; the reference only assumes its size, quantization.rs:122):
+ *   element i of an n-element, b-bit tensor occupies bits [i*b, (i+1)*b) of a little-endian
+ *   bitstream, i.e. byte (i*b)/8 from bit (i*b)%8 upward (spilling into the next byte when
+ *   b does not divide 8); total ceil(n*b/8) bytes; unused high bits of the last byte are 0.
+ */
+#ifndef DLLM_QUANT_H
+#define DLLM_QUANT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void *dllm_stream_t; /* hipStream_t */
+
+enum dllm_status {
+    DLLM_OK = 0,
+    DLLM_ERR_INVALID_PARAMS = 1,        /* QuantizationError::InvalidParams + reference panics */
+    DLLM_ERR_UNSUPPORTED = 2,           /* QuantizationError::UnsupportedOperation */
+    DLLM_ERR_SHAPE_MISMATCH = 3,        /* QuantizationError::ShapeMismatch */
+    DLLM_ERR_CALIBRATION_REQUIRED = 4,  /* QuantizationError::CalibrationRequired */
+    DLLM_ERR_IO = 5,                    /* QuantizationError::Io */
+    DLLM_ERR_SERIALIZATION = 6,         /* QuantizationError::Serialization */
+    DLLM_ERR_INVALID_DATA_FORMAT = 7,   /* QuantizationError::InvalidDataFormat */
+    DLLM_ERR_HIP = 16,                  /* a HIP runtime call failed */
+    DLLM_ERR_NO_DEVICE = 17,            /* no gfx950 device visible */
+};
+
+enum dllm_dtype { DLLM_F32 = 0, DLLM_F16 = 1 };
+
+/* quantization/src/quantize.rs:62-67 QuantizationType */
+enum dllm_qtype { DLLM_QT_INT8 = 0, DLLM_QT_INT4 = 1, DLLM_QT_BINARY = 2, DLLM_QT_FLOAT8 = 3 };
+
+/* ---- library ---------------------------------------------------------------------------- */
+const char *dllm_last_error(void);  /* thread-local message of the last failing call */
+const char *dllm_version(void);
+int dllm_device_arch(int device, char *buf, size_t len); /* gcnArchName, e.g. "gfx950:sramecc+:xnack-" */
+
+/* ---- a1 / a2: diffuse-llm-rs/src/quantization.rs --------------------------------------- */
+
+/* Bytes of device workspace dllm_quantize_tensor needs for n elements. */
+size_t dllm_quantize_tensor_workspace(size_t n);
+
+/* quantize_tensor(data: &[f32], bits: u8) -> (Vec<u8>, f32, f32)   (quantization.rs:38-68)
+ * Per-tensor asymmetric quantization: global min/max, scale = (max-min)/(2^bits-1) (1.0 if 0),
+ * zp = round(clamp(0 - min/scale, 0, 2^bits-1)) as u8, q = clamp(round(x/scale + zp), 0, 2^bits-1).
+ * x[n] f32; out: n bytes (packed=0) or ceil(n*bits/8) bytes (packed=1);
+ * params_out[2] = {scale, zero_point as f32} written on the device (no host sync).
+ * bits outside 1..=8 -> DLLM_ERR_INVALID_PARAMS (the reference's assert!, quantization.rs:39). */
+int dllm_quantize_tensor(const float *x, size_t n, uint8_t bits, int packed, uint8_t *out, float *params_out,
+                         void *workspace, size_t workspace_bytes, dllm_stream_t stream);
+
+/* dequantize_tensor(data: &[u8], scale: f32, zero_point: f32) -> Vec<f32> (quantization.rs:81-85)
+ * and QuantizedTensor::dequantize (:115-117):  y = ((q as f32) - zp) * scale.
+ * params[2] = {scale, zp} in DEVICE memory (as written by dllm_quantize_tensor).
+ * out_dtype DLLM_F32 gives the reference's f32 bits exactly; DLLM_F16 = that f32 rounded (RNE). */
+int dllm_dequantize_tensor(const uint8_t *q, size_t n, uint8_t bits, int packed, const float *params,
+                           void *out, int out_dtype, dllm_stream_t stream);
+/* Same with host scalars (dequantize_tensor's literal signature). */
+int dllm_dequantize_tensor_scalar(const uint8_t *q, size_t n, uint8_t bits, int packed, float scale, float zp,
+                                  void *out, int out_dtype, dllm_stream_t stream);
+
+/* QuantizedTensor::compression_ratio (quantization.rs:120-124); host-only arithmetic. */
+float dllm_compression_ratio(size_t numel, size_t len, uint8_t bits);
+
+/* ---- a6: pack / unpack (build-defined layout above) -------------------------------------- */
+size_t dllm_packed_bytes(size_t n, uint8_t bits);
+int dllm_pack(const uint8_t *codes, size_t n, uint8_t bits, uint8_t *packed, dllm_stream_t stream);
+int dllm_unpack(const uint8_t *packed, size_t n, uint8_t bits, uint8_t *codes, dllm_stream_t stream);
+
+/* ---- a4: quantization crate DefaultQuantizer ---------------------------------------------
+ * trait Quantizer::quantize / dequantize (quantization/src/quantize.rs:81-90) as implemented by
+ * DefaultQuantizer (:98-184) and quant_utils::{quantize, dequantize} (:191-215):
+ *   q = (round(min(max(x/scale + zp, lo), hi)) as u8), (lo,hi) by qtype (:139-144);
+ *   y = (q as f32 - zp) * scale.  One code per byte (the reference's QuantizedTensor::data). */
+int dllm_default_quantize(const float *x, size_t n, int qtype, float scale, int32_t zero_point, uint8_t *out,
+                          dllm_stream_t stream);
+int dllm_default_dequantize(const uint8_t *q, size_t n, float scale, int32_t zero_point, float *out,
+                            dllm_stream_t stream);
+
+/* ---- a10: calibration (quantization/src/calibrate.rs:42-110) ------------------------------
+ * Device-side CalibrationData::update reduction: stats[2] = {min, max} folded into the running
+ * values (initialise to {f32::MAX, f32::MIN}), histogram[num_bins] (u64) accumulated for the
+ * updated range exactly as calibrate.rs:58-68.  compute_params is host arithmetic. */
+int dllm_calib_update(const float *x, size_t n, float *stats, uint64_t *histogram, size_t num_bins,
+                      void *workspace, size_t workspace_bytes, dllm_stream_t stream);
+int dllm_calib_compute_params(float min, float max, size_t total_samples, uint8_t bits, int symmetric,
+                              float *scale, int32_t *zero_point);
+
+/* ---- a8-ii: prefill-kvquant-rs kvquant::BitQuantizer (prefill-kvquant-rs/lib.rs:29-53) ------
+ * quantize: q = ((x - zp) / scale).clamp(0, (1<<bits)-1) as u8  (truncation, no rounding);
+ * dequantize: y = q as f32 * scale + zp.  bits > 30 -> INVALID_PARAMS (i32 shift overflow). */
+int dllm_bit_quantize(const float *x, size_t n, uint32_t bits, float scale, float zero_point, uint8_t *out,
+                      dllm_stream_t stream);
+int dllm_bit_dequantize(const uint8_t *q, size_t n, float scale, float zero_point, void *out, int out_dtype,
+                        dllm_stream_t stream);
+
+/* PrefillKVQuant::quantize_vectors (prefill-kvquant-rs/lib.rs:127-146) over `rows` token vectors of
+ * `dim` values: row r uses bits req_bits[r % nreq] and quantizers[bits/2] built by
+ * PrefillKVQuant::new from cfg_bits (:101-110).  cfg_bits/req_bits are HOST arrays (the config);
+ * x/out DEVICE.  out_bits[rows] (host) receives CompressedVector::bits.  bits/2 >= ncfg -> the
+ * reference panics -> INVALID_PARAMS, nothing launched. */
+int dllm_quantize_vectors(const float *x, size_t rows, size_t dim, const uint8_t *cfg_bits, size_t ncfg,
+                          const uint8_t *req_bits, size_t nreq, uint8_t *out, uint8_t *out_bits,
+                          dllm_stream_t stream);
+
+/* ---- a8-iii: diffusion_prefill KVCache::compress_vector / decompress_vector -----------------
+ * (diffusion_prefill/src/prefill_kv.rs:104-132), batched over rows: per row min/max,
+ * scale = (max-min)/(2^bits-1), zp = min, BitQuantizer.  scales/zps [rows] device. */
+int dllm_compress_vectors(const float *x, size_t rows, size_t dim, uint8_t bits, uint8_t *out, float *scales,
+                          float *zps, dllm_stream_t stream);
+int dllm_decompress_vectors(const uint8_t *q, size_t rows, size_t dim, const float *scales, const float *zps,
+                            float *out, dllm_stream_t stream);
+
+/* ---- a5: group-quantized linear layer ---------------------------------------------------
+ * Replaces SimpleDiffusionModel::forward = x.dot(W) + b (diffuse-llm-rs/src/lib.rs:806-813),
+ * W [K, N] ("[input_dim, output_dim]", :776-777), with W quantized per (output column n, K-group g
+ * of `group` rows) by quantize_tensor (a1, bits in {2,4,8}) and dequantized by a2 inside the
+ * GEMM.  group = QuantizationConfig::default().group_size = 128 (quantization/src/types.rs:124-127).
+ * Device compute: dequantized weight rounded to f16, f16 MFMA with f32 accumulation, bias in f32.
+ * Requirements: K % 64 == 0, group % 64 == 0; any M >= 0, any N >= 1. */
+typedef struct dllm_linear *dllm_linear_t;
+
+/* W (device, f32 [K][N] row-major), bias (device f32 [N] or NULL = zeros, the reference's
+ * Array1::zeros, lib.rs:798).  Quantization runs on the GPU (bit-exact with a1). */
+int dllm_linear_create(const float *W, const float *bias, size_t K, size_t N, uint8_t bits, size_t group,
+                       dllm_linear_t *out, dllm_stream_t stream);
+/* Import already-quantized weights: codes packed in the canonical bitstream of the [K][N]
+ * row-major code matrix, scales f32 [G][N], zps u8 [G][N] (G = ceil(K/group)); all device. */
+int dllm_linear_create_quantized(const uint8_t *packed_codes, const float *scales, const uint8_t *zps,
+                                 const float *bias, size_t K, size_t N, uint8_t bits, size_t group,
+                                 dllm_linear_t *out, dllm_stream_t stream);
+/* Y[M][ldy] = X[M][K] . W^ + b.  x_dtype/y_dtype in {DLLM_F32, DLLM_F16}; an f32 X is cast to f16
+ * through a workspace owned by the handle (grown outside stream capture, before the launch). */
+int dllm_linear_forward(dllm_linear_t h, const void *X, size_t M, int x_dtype, void *Y, int y_dtype,
+                        dllm_stream_t stream);
+/* Export the quantized weights in canonical form (packed bitstream [K][N], scales [G][N], zps). */
+int dllm_linear_export(dllm_linear_t h, uint8_t *packed_codes, float *scales, uint8_t *zps,
+                       dllm_stream_t stream);
+int dllm_linear_info(dllm_linear_t h, size_t *K, size_t *N, uint8_t *bits, size_t *group);
+/* HBM bytes the forward's GEMM kernel reads for the weights (packed codes + scales/zps). */
+size_t dllm_linear_weight_bytes(dllm_linear_t h);
+int dllm_linear_destroy(dllm_linear_t h);
+
+/* ---- a9: int-quantized KV dequant-attention (consumer of QuantizedKVCacheEntry) -------------
+ * The reference dequantizes K/V (QuantizedKVCacheEntry::dequantize_keys/values,
+ * diffuse-llm-rs/src/quantization.rs:160-175) and hands them to DiffusionModel::forward_with_cache
+ * (diffuse-llm-rs/src/lib.rs:910-915).  Build-defined consumer: per head, bidirectional SDPA
+ * O = softmax(Q K^T / sqrt(D)) V, with K,V given as per-tensor quantized codes (a1 layout,
+ * packed, `bits` in {4, 8}) + device params {scale, zp} (a2 dequant fused into the kernel).
+ * Q f16 [S][H][D], O f16 [S][H][D], D == 128. */
+int dllm_kv_attention(const void *Q, const uint8_t *Kq, const float *k_params, const uint8_t *Vq,
+                      const float *v_params, uint8_t bits, size_t S, size_t H, size_t D, void *O,
+                      dllm_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DLLM_QUANT_H */

@@ -1,0 +1,194 @@
+"""ctypes binding of the C oracle (oracle/_build/liborc.so).
+
+TEST INFRASTRUCTURE ONLY: the parity checker and the CPU baseline.  Only tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg import this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "_build" / "liborc.so"
+
+_lib = None
+
+
+def build(force: bool = False) -> Path:
+    src = HERE / "dllm_oracle.c"
+    if force or not LIB_PATH.exists() or LIB_PATH.stat().st_mtime < src.stat().st_mtime:
+        subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = C.CDLL(str(LIB_PATH))
+        P, S, F, U8, I32 = C.c_void_p, C.c_size_t, C.c_float, C.c_uint8, C.c_int32
+        sig = {
+            "orc_quantize_tensor": (C.c_int, [P, S, U8, P, P, P]),
+            "orc_dequantize_tensor": (None, [P, S, F, F, P]),
+            "orc_compression_ratio": (F, [S, S, U8]),
+            "orc_packed_bytes": (S, [S, U8]),
+            "orc_pack_bits": (C.c_int, [P, S, U8, P]),
+            "orc_unpack_bits": (C.c_int, [P, S, U8, P]),
+            "orc_default_quantize": (C.c_int, [P, S, C.c_int, F, I32, P]),
+            "orc_default_dequantize": (None, [P, S, F, I32, P]),
+            "orc_bit_quantize": (C.c_int, [P, S, C.c_uint32, F, F, P]),
+            "orc_bit_dequantize": (None, [P, S, F, F, P]),
+            "orc_prefill_scale": (C.c_int, [C.c_uint32, P]),
+            "orc_quantize_vectors": (C.c_int, [P, S, S, P, S, P, S, P, P]),
+            "orc_compress_vector": (C.c_int, [P, S, U8, P, P, P]),
+            "orc_quantize_weights": (C.c_int, [P, S, S, U8, S, P, P, P]),
+            "orc_dequantize_weights": (None, [P, P, P, S, S, S, P]),
+            "orc_linear_forward": (None, [P, S, S, P, S, P, P, C.c_int]),
+            "orc_attention": (None, [P, P, P, S, S, S, P, S, C.c_int]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype, fn.argtypes = res, args
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+class OracleError(RuntimeError):
+    pass
+
+
+def _check(rc):
+    if rc != 0:
+        raise OracleError(f"oracle returned {rc}")
+
+
+def quantize_tensor(x: np.ndarray, bits: int):
+    x = np.ascontiguousarray(x, np.float32).ravel()
+    q = np.zeros(x.size, np.uint8)
+    s, z = C.c_float(), C.c_float()
+    _check(lib().orc_quantize_tensor(_p(x), x.size, bits, _p(q), C.byref(s), C.byref(z)))
+    return q, np.float32(s.value), np.float32(z.value)
+
+
+def dequantize_tensor(q, scale, zp):
+    q = np.ascontiguousarray(q, np.uint8).ravel()
+    out = np.zeros(q.size, np.float32)
+    lib().orc_dequantize_tensor(_p(q), q.size, float(scale), float(zp), _p(out))
+    return out
+
+
+def pack_bits(codes, bits):
+    codes = np.ascontiguousarray(codes, np.uint8).ravel()
+    out = np.zeros(lib().orc_packed_bytes(codes.size, bits), np.uint8)
+    _check(lib().orc_pack_bits(_p(codes), codes.size, bits, _p(out)))
+    return out
+
+
+def unpack_bits(packed, n, bits):
+    packed = np.ascontiguousarray(packed, np.uint8).ravel()
+    out = np.zeros(n, np.uint8)
+    _check(lib().orc_unpack_bits(_p(packed), n, bits, _p(out)))
+    return out
+
+
+def default_quantize(x, qtype, scale=1.0, zero_point=0):
+    x = np.ascontiguousarray(x, np.float32).ravel()
+    out = np.zeros(x.size, np.uint8)
+    _check(lib().orc_default_quantize(_p(x), x.size, qtype, scale, zero_point, _p(out)))
+    return out
+
+
+def default_dequantize(q, scale=1.0, zero_point=0):
+    q = np.ascontiguousarray(q, np.uint8).ravel()
+    out = np.zeros(q.size, np.float32)
+    lib().orc_default_dequantize(_p(q), q.size, scale, zero_point, _p(out))
+    return out
+
+
+def bit_quantize(x, bits, scale, zero_point):
+    x = np.ascontiguousarray(x, np.float32).ravel()
+    out = np.zeros(x.size, np.uint8)
+    _check(lib().orc_bit_quantize(_p(x), x.size, bits, scale, zero_point, _p(out)))
+    return out
+
+
+def bit_dequantize(q, scale, zero_point):
+    q = np.ascontiguousarray(q, np.uint8).ravel()
+    out = np.zeros(q.size, np.float32)
+    lib().orc_bit_dequantize(_p(q), q.size, scale, zero_point, _p(out))
+    return out
+
+
+def prefill_scale(bits):
+    s = C.c_float()
+    _check(lib().orc_prefill_scale(bits, C.byref(s)))
+    return np.float32(s.value)
+
+
+def quantize_vectors(x, cfg_bits, req_bits):
+    x = np.ascontiguousarray(x, np.float32)
+    rows, dim = x.shape
+    cfg = np.ascontiguousarray(cfg_bits, np.uint8)
+    req = np.ascontiguousarray(req_bits, np.uint8)
+    out = np.zeros((rows, dim), np.uint8)
+    widths = np.zeros(rows, np.uint8)
+    _check(lib().orc_quantize_vectors(_p(x), rows, dim, _p(cfg), cfg.size, _p(req), req.size, _p(out),
+                                      _p(widths)))
+    return out, widths
+
+
+def compress_vector(x, bits):
+    x = np.ascontiguousarray(x, np.float32).ravel()
+    out = np.zeros(x.size, np.uint8)
+    s, z = C.c_float(), C.c_float()
+    _check(lib().orc_compress_vector(_p(x), x.size, bits, _p(out), C.byref(s), C.byref(z)))
+    return out, np.float32(s.value), np.float32(z.value)
+
+
+def quantize_weights(W, bits=4, group=128):
+    W = np.ascontiguousarray(W, np.float32)
+    K, N = W.shape
+    G = (K + group - 1) // group
+    codes = np.zeros((K, N), np.uint8)
+    scales = np.zeros((G, N), np.float32)
+    zps = np.zeros((G, N), np.uint8)
+    _check(lib().orc_quantize_weights(_p(W), K, N, bits, group, _p(codes), _p(scales), _p(zps)))
+    return codes, scales, zps
+
+
+def dequantize_weights(codes, scales, zps, group=128):
+    codes = np.ascontiguousarray(codes, np.uint8)
+    K, N = codes.shape
+    out = np.zeros((K, N), np.float32)
+    lib().orc_dequantize_weights(_p(codes), _p(np.ascontiguousarray(scales, np.float32)),
+                                 _p(np.ascontiguousarray(zps, np.uint8)), K, N, group, _p(out))
+    return out
+
+
+def linear_forward(X, W, bias=None, nthreads=1):
+    X = np.ascontiguousarray(X, np.float32)
+    W = np.ascontiguousarray(W, np.float32)
+    M, K = X.shape
+    N = W.shape[1]
+    Y = np.zeros((M, N), np.float32)
+    b = None if bias is None else np.ascontiguousarray(bias, np.float32)
+    lib().orc_linear_forward(_p(X), M, K, _p(W), N, None if b is None else _p(b), _p(Y), nthreads)
+    return Y
+
+
+def attention(Q, K, V, q_rows=None, nthreads=None):
+    Q, K, V = (np.ascontiguousarray(a, np.float32) for a in (Q, K, V))
+    S, H, D = Q.shape
+    q_rows = S if q_rows is None else q_rows
+    O = np.zeros((q_rows, H, D), np.float32)
+    nthreads = nthreads or (os.cpu_count() or 1)
+    lib().orc_attention(_p(Q), _p(K), _p(V), S, H, D, _p(O), q_rows, nthreads)
+    return O

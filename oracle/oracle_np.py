@@ -1,0 +1,266 @@
+"""Independent numpy restatement of the reference's quantized hot path.
+
+TEST INFRASTRUCTURE ONLY.  Written separately from ``dllm_oracle.c`` so the two restatements can
+cross-check each other bit for bit.  Used by ``tests/golden/make_golden.py``
+to produce the committed golden vectors and by the CPU test-suite; never imported by the product.
+
+All arithmetic is float32 with one rounding per operation (numpy never fuses), matching Rust f32.
+Each function cites the Rust code it restates (paths relative to the reference root).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+F32 = np.float32
+
+
+def rs_round(x: np.ndarray) -> np.ndarray:
+    """Rust ``f32::round``: half away from zero (numpy's ``round`` is half-to-even)."""
+    x = np.asarray(x, dtype=F32)
+    t = np.trunc(x)
+    with np.errstate(invalid="ignore"):
+        frac = np.abs(x - t)
+        up = frac >= F32(0.5)
+    return np.where(up, t + np.sign(x).astype(F32), t).astype(F32)
+
+
+def rs_as_u8(x: np.ndarray) -> np.ndarray:
+    """Rust ``f as u8``: saturating, truncating, NaN -> 0."""
+    x = np.asarray(x, dtype=F32)
+    with np.errstate(invalid="ignore"):
+        out = np.where(np.isnan(x) | (x <= 0), F32(0), np.where(x >= 255, F32(255), np.trunc(x)))
+    return out.astype(np.uint8)
+
+
+def rs_as_i32(x: np.ndarray) -> np.ndarray:
+    x = np.asarray(x, dtype=np.float64)  # exact widening
+    with np.errstate(invalid="ignore"):
+        out = np.where(np.isnan(x), 0.0, np.clip(np.trunc(x), -2147483648.0, 2147483647.0))
+    return out.astype(np.int64)
+
+
+def rs_clamp(x: np.ndarray, lo: float, hi: float) -> np.ndarray:
+    """Rust ``f32::clamp``: NaN passes through."""
+    x = np.asarray(x, dtype=F32)
+    with np.errstate(invalid="ignore"):
+        x = np.where(x < F32(lo), F32(lo), x)
+        x = np.where(x > F32(hi), F32(hi), x)
+    return x.astype(F32)
+
+
+def fold_max(x: np.ndarray) -> F32:
+    return F32(np.fmax.reduce(np.asarray(x, F32).ravel(), initial=-np.inf))
+
+
+def fold_min(x: np.ndarray) -> F32:
+    return F32(np.fmin.reduce(np.asarray(x, F32).ravel(), initial=np.inf))
+
+
+# ---- a1 / a2: diffuse-llm-rs/src/quantization.rs -------------------------------------------
+
+def quantize_tensor(data: np.ndarray, bits: int):
+    """quantization.rs:38-68 -> (codes u8, scale f32, zero_point f32)."""
+    if not 1 <= bits <= 8:
+        raise ValueError("Bits must be between 1 and 8")  # :39 assert!
+    x = np.asarray(data, dtype=F32).ravel()
+    mx, mn = fold_max(x), fold_min(x)
+    q_min, q_max = F32(0.0), F32(float(1 << bits) - 1.0)
+    with np.errstate(all="ignore"):
+        scale = F32((mx - mn) / (q_max - q_min))
+        if scale == F32(0.0):
+            scale = F32(1.0)
+        zpf = F32(q_min - F32(mn / scale))
+        zp = rs_as_u8(rs_round(rs_clamp(np.array([zpf], F32), q_min, q_max)))[0]
+        v = (x / scale).astype(F32)
+        v = (v + F32(zp)).astype(F32)
+        q = np.clip(rs_as_i32(rs_round(v)), 0, (1 << bits) - 1).astype(np.uint8)
+    return q, F32(scale), F32(zp)
+
+
+def dequantize_tensor(q: np.ndarray, scale, zero_point) -> np.ndarray:
+    """quantization.rs:81-85."""
+    d = (np.asarray(q).astype(F32) - F32(zero_point)).astype(F32)
+    return (d * F32(scale)).astype(F32)
+
+
+def compression_ratio(numel: int, length: int, bits: int) -> float:
+    """quantization.rs:120-124."""
+    return float(F32(numel * 4) / F32((length * bits + 7) // 8))
+
+
+# ---- a6: build-defined LSB-first packing ----------------------------------------------------
+
+def pack_bits(codes: np.ndarray, bits: int) -> np.ndarray:
+    codes = np.asarray(codes, np.uint8).ravel().astype(np.uint64) & ((1 << bits) - 1)
+    n = codes.size
+    nbytes = (n * bits + 7) // 8
+    bitpos = np.arange(n, dtype=np.uint64) * bits
+    out = np.zeros(nbytes + 1, dtype=np.uint64)
+    lo = (codes << (bitpos & 7)) & 0xFF
+    hi = (codes << (bitpos & 7)) >> 8
+    np.bitwise_or.at(out, (bitpos >> 3).astype(np.int64), lo)
+    np.bitwise_or.at(out, ((bitpos >> 3) + 1).astype(np.int64), hi)
+    return out[:nbytes].astype(np.uint8)
+
+
+def unpack_bits(packed: np.ndarray, n: int, bits: int) -> np.ndarray:
+    p = np.concatenate([np.asarray(packed, np.uint8).ravel(), np.zeros(1, np.uint8)]).astype(np.uint64)
+    bitpos = np.arange(n, dtype=np.uint64) * bits
+    idx = (bitpos >> 3).astype(np.int64)
+    v = p[idx] | (p[idx + 1] << 8)
+    return ((v >> (bitpos & 7)) & ((1 << bits) - 1)).astype(np.uint8)
+
+
+# ---- a4: quantization/src/quantize.rs DefaultQuantizer -------------------------------------
+
+QTYPE_RANGE = {0: (-128.0, 127.0), 1: (-8.0, 7.0), 2: (0.0, 1.0), 3: (-127.0, 127.0)}  # :139-144
+QTYPE_BITS = {0: 8, 1: 4, 2: 1, 3: 8}  # :69-78
+
+
+def default_quantize(x: np.ndarray, qtype: int, scale=1.0, zero_point=0) -> np.ndarray:
+    """quantize.rs:111-154 (quantize_value then ``q as u8``)."""
+    lo, hi = QTYPE_RANGE[qtype]
+    x = np.asarray(x, F32).ravel()
+    with np.errstate(all="ignore"):
+        v = (x / F32(scale)).astype(F32)
+        v = (v + F32(zero_point)).astype(F32)
+        v = np.fmin(np.fmax(v, F32(lo)), F32(hi)).astype(F32)
+    return rs_as_u8(rs_round(v))
+
+
+def default_dequantize(q: np.ndarray, scale=1.0, zero_point=0) -> np.ndarray:
+    """quantize.rs:172-184."""
+    return dequantize_tensor(q, F32(scale), F32(zero_point))
+
+
+# ---- a8-ii: prefill-kvquant-rs/lib.rs BitQuantizer ----------------------------------------
+
+def bit_quantize(x: np.ndarray, bits: int, scale, zero_point) -> np.ndarray:
+    """lib.rs:40-46 (truncation, no rounding)."""
+    max_val = F32((1 << bits) - 1)
+    with np.errstate(all="ignore"):
+        s = ((np.asarray(x, F32).ravel() - F32(zero_point)).astype(F32) / F32(scale)).astype(F32)
+    return rs_as_u8(rs_clamp(s, F32(0.0), max_val))
+
+
+def bit_dequantize(q: np.ndarray, scale, zero_point) -> np.ndarray:
+    """lib.rs:48-52."""
+    p = (np.asarray(q).astype(F32) * F32(scale)).astype(F32)
+    return (p + F32(zero_point)).astype(F32)
+
+
+def prefill_scale(cfg_bits: int) -> F32:
+    """lib.rs:104-108."""
+    return F32(F32(1.0) / F32((1 << cfg_bits) - 1))
+
+
+def quantize_vectors(x: np.ndarray, cfg_bits, req_bits):
+    """lib.rs:127-146 over rows of x [rows, dim]."""
+    out, widths = [], []
+    if len(req_bits) == 0:
+        return np.zeros((0, x.shape[1]), np.uint8), np.zeros(0, np.uint8)
+    for r in range(x.shape[0]):
+        b = int(req_bits[r % len(req_bits)])
+        qi = b // 2
+        if qi >= len(cfg_bits):
+            raise IndexError("quantizers[bits / 2] out of bounds")
+        out.append(bit_quantize(x[r], b, prefill_scale(int(cfg_bits[qi])), 0.0))
+        widths.append(b)
+    return np.stack(out), np.array(widths, np.uint8)
+
+
+# ---- a8-iii: diffusion_prefill/src/prefill_kv.rs compress_vector ---------------------------
+
+def compress_vector(x: np.ndarray, bits: int):
+    """prefill_kv.rs:104-121."""
+    x = np.asarray(x, F32).ravel()
+    mn, mx = fold_min(x), fold_max(x)
+    levels = F32((1 << bits) - 1)
+    with np.errstate(all="ignore"):
+        scale = F32((mx - mn) / levels)
+        s = ((x - mn).astype(F32) / scale).astype(F32)
+    return rs_as_u8(rs_clamp(s, F32(0.0), levels)), scale, F32(mn)
+
+
+# ---- a10: quantization/src/calibrate.rs ------------------------------------------------------
+
+class Calibration:
+    """calibrate.rs:19-110."""
+
+    F32_MAX = F32(3.40282347e38)
+
+    def __init__(self, num_bins: int):
+        self.min, self.max = self.F32_MAX, -self.F32_MAX
+        self.num_bins = num_bins
+        self.histogram = np.zeros(num_bins, np.uint64)
+        self.total_samples = 0
+
+    def update(self, data: np.ndarray):
+        x = np.asarray(data, F32).ravel()
+        mn = F32(np.fmin.reduce(x, initial=self.F32_MAX))
+        mx = F32(np.fmax.reduce(x, initial=-self.F32_MAX))
+        self.min, self.max = F32(np.fmin(self.min, mn)), F32(np.fmax(self.max, mx))
+        self.total_samples += x.size
+        if self.max > self.min:
+            bw = F32((self.max - self.min) / F32(self.num_bins))
+            sel = x[(x >= self.min) & (x <= self.max)]
+            b = np.floor(((sel - self.min).astype(F32) / bw).astype(F32))
+            b = np.minimum(np.where(b <= 0, 0, b).astype(np.int64), self.num_bins - 1)
+            np.add.at(self.histogram, b, 1)
+
+    def compute_params(self, bits: int, symmetric: bool):
+        if self.total_samples == 0:
+            raise RuntimeError("CalibrationRequired")
+        nl = F32(2 ** bits)
+        rng = F32(self.max - self.min)
+        if rng <= F32(1.1920929e-07):
+            return F32(1.0), 0
+        if symmetric:
+            ma = F32(max(abs(self.max), abs(self.min)))
+            scale = F32(F32(ma * F32(2.0)) / F32(nl - F32(1.0)))
+            zp = int(rs_as_i32(np.array([F32(nl / F32(2.0)) - F32(1.0)], F32))[0])
+        else:
+            scale = F32(rng / F32(nl - F32(1.0)))
+            zp = int(rs_as_i32(rs_round(np.array([F32(-self.min) / scale], F32)))[0])
+        return scale, zp
+
+
+# ---- a5: group-wise weight quantization + linear layer --------------------------------------
+
+def quantize_weights(W: np.ndarray, bits: int = 4, group: int = 128):
+    """Per (column, K-group) quantize_tensor -> codes [K,N], scales [G,N], zps [G,N]."""
+    K, N = W.shape
+    G = (K + group - 1) // group
+    codes = np.zeros((K, N), np.uint8)
+    scales = np.zeros((G, N), F32)
+    zps = np.zeros((G, N), np.uint8)
+    for g in range(G):
+        blk = np.asarray(W[g * group:(g + 1) * group], F32)
+        mx = np.fmax.reduce(blk, axis=0, initial=-np.inf).astype(F32)
+        mn = np.fmin.reduce(blk, axis=0, initial=np.inf).astype(F32)
+        q_max = F32(float(1 << bits) - 1.0)
+        with np.errstate(all="ignore"):
+            s = ((mx - mn).astype(F32) / q_max).astype(F32)
+            s = np.where(s == 0, F32(1.0), s).astype(F32)
+            zpf = (F32(0.0) - (mn / s).astype(F32)).astype(F32)
+            z = rs_as_u8(rs_round(rs_clamp(zpf, 0.0, q_max)))
+            v = (blk / s[None, :]).astype(F32)
+            v = (v + z.astype(F32)[None, :]).astype(F32)
+        codes[g * group:(g + 1) * group] = np.clip(rs_as_i32(rs_round(v)), 0, (1 << bits) - 1)
+        scales[g], zps[g] = s, z
+    return codes, scales, zps
+
+
+def dequantize_weights(codes, scales, zps, group: int = 128) -> np.ndarray:
+    K = codes.shape[0]
+    g = np.arange(K) // group
+    d = (codes.astype(F32) - zps[g].astype(F32)).astype(F32)
+    return (d * scales[g]).astype(F32)
+
+
+def linear_forward(X: np.ndarray, W: np.ndarray, bias=None) -> np.ndarray:
+    """diffuse-llm-rs/src/lib.rs:806-813 (accumulated in f64, returned f32)."""
+    Y = np.asarray(X, np.float64) @ np.asarray(W, np.float64)
+    if bias is not None:
+        Y = Y + np.asarray(bias, np.float64)[None, :]
+    return Y.astype(F32)

@@ -1,0 +1,43 @@
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+if str(ROOT) not in sys.path:
+    sys.path.insert(0, str(ROOT))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU; run with -m gpu")
+
+
+@pytest.fixture(scope="session")
+def orc():
+    """The C oracle (parity checker)."""
+    from oracle import oracle
+    oracle.build()
+    return oracle
+
+
+@pytest.fixture(scope="session")
+def onp():
+    from oracle import oracle_np
+    return oracle_np
+
+
+@pytest.fixture(scope="session")
+def dllm():
+    """The product package (HIP path).  Fails loudly if the library is missing."""
+    import __graft_entry__ as g
+    mod = g.load_package()
+    mod.load_library()
+    return mod
+
+
+@pytest.fixture(scope="session")
+def cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("-m gpu test run without a visible GPU")
+    return torch.device("cuda")

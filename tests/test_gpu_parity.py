@@ -1,0 +1,293 @@
+"""GPU parity: every HIP kernel through the C-ABI vs the oracle / golden vectors.
+
+Bar: bit-exact for codes, packed bytes and the f32 outputs of a1/a2/a4/a8/a10; the GEMM within
+``REL_TOL`` relative Frobenius error of the f32 CPU restatement (north_star: 1e-3).
+"""
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = Path(__file__).resolve().parent / "golden" / "golden_v1.npz"
+REL_TOL = 1e-3  # north_star: "outputs within 1e-3 rel-err of the CPU reference"
+
+
+@pytest.fixture(scope="module")
+def gold():
+    with np.load(GOLDEN, allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+@pytest.fixture(scope="module")
+def torch(cuda):
+    import torch as t
+    return t
+
+
+def dev(torch, a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    return t if dtype is None else t.to(dtype)
+
+
+def host(t):
+    return t.detach().cpu().numpy()
+
+
+def same_bits(a, b):
+    return np.ascontiguousarray(a).view(np.uint8).tobytes() == np.ascontiguousarray(b).view(np.uint8).tobytes()
+
+
+def rel_err(y, ref):
+    ref = np.asarray(ref, np.float64)
+    return float(np.linalg.norm(np.asarray(y, np.float64) - ref) / np.linalg.norm(ref))
+
+
+# ---- a1 / a2 / a6 ------------------------------------------------------------------------------
+
+def test_quantize_tensor_golden(dllm, torch, gold):
+    names = sorted({k.split("/")[1] for k in gold if k.startswith("a1/")})
+    for name in names:
+        x = gold[f"a1/{name}/x"]
+        for bits in range(1, 9):
+            for packed in (False, True):
+                q, params = dllm.quantize_tensor(dev(torch, x), bits, packed=packed)
+                exp = gold[f"a1/{name}/b{bits}/packed" if packed else f"a1/{name}/b{bits}/q"]
+                assert np.array_equal(host(q), exp), (name, bits, packed)
+                assert same_bits(host(params), gold[f"a1/{name}/b{bits}/params"]), (name, bits)
+                y = dllm.dequantize_tensor(q, params, bits=bits, packed=packed, n=x.size)
+                assert same_bits(host(y), gold[f"a1/{name}/b{bits}/deq"]), (name, bits, packed)
+
+
+def test_quantize_tensor_random_sizes(dllm, torch, orc):
+    """Ragged sizes (odd tails, every octet remainder) and unaligned base pointers."""
+    rng = np.random.default_rng(7)
+    for n in [1, 7, 8, 9, 63, 64, 65, 1000, 4097, 100_003, 1 << 20]:
+        x = (rng.standard_normal(n + 3) * rng.uniform(0.1, 10)).astype(np.float32)
+        xd = dev(torch, x)
+        for off in (0, 1, 3):
+            xs = x[off:off + n]
+            for bits in (1, 2, 3, 4, 5, 8):
+                q, params = dllm.quantize_tensor(xd[off:off + n], bits, packed=True)
+                rq, rs, rz = orc.quantize_tensor(xs, bits)
+                assert np.array_equal(host(q), orc.pack_bits(rq, bits)), (n, off, bits)
+                assert same_bits(host(params), np.array([rs, rz], np.float32))
+                for dt in (torch.float32, torch.float16):
+                    y = dllm.dequantize_tensor(q, params, bits=bits, packed=True, n=n, out_dtype=dt)
+                    ref = orc.dequantize_tensor(rq, rs, rz)
+                    if dt == torch.float32:
+                        assert same_bits(host(y), ref)
+                    else:
+                        assert same_bits(host(y), ref.astype(np.float16))
+
+
+def test_dequantize_scalar_signature(dllm, torch, orc):
+    rng = np.random.default_rng(1)
+    q = rng.integers(0, 16, 777).astype(np.uint8)
+    y = dllm.dequantize_tensor(dev(torch, q), 0.123, 7.0)
+    assert same_bits(host(y), orc.dequantize_tensor(q, np.float32(0.123), np.float32(7.0)))
+
+
+def test_pack_unpack_golden(dllm, torch, gold):
+    for bits in range(1, 9):
+        c = gold[f"a6/b{bits}/codes"]
+        p = dllm.pack(dev(torch, c), bits)
+        assert np.array_equal(host(p), gold[f"a6/b{bits}/packed"])
+        assert np.array_equal(host(dllm.unpack(p, c.size, bits)), c)
+
+
+def test_quantized_kv_cache_entry(dllm, torch, orc):
+    """quantization.rs:128-176 on a [layers, seq, hidden] cache: per-tensor K and V params."""
+    rng = np.random.default_rng(11)
+    K = rng.standard_normal((2, 96, 256)).astype(np.float32)
+    V = (rng.standard_normal((2, 96, 256)) * 3 + 1).astype(np.float32)
+    e = dllm.QuantizedKVCacheEntry.new(dev(torch, K), dev(torch, V), 4)
+    assert e.seq_len == 96
+    for t, ref in ((e.dequantize_keys(), K), (e.dequantize_values(), V)):
+        rq, rs, rz = orc.quantize_tensor(ref, 4)
+        assert same_bits(host(t).ravel(), orc.dequantize_tensor(rq, rs, rz))
+    assert e.keys.compression_ratio() == pytest.approx(8.0)
+    assert e.memory_usage() == 2 * (K.size * 4 + 7) // 8
+
+
+# ---- a4 -----------------------------------------------------------------------------------------
+
+def test_default_quantizer_golden(dllm, torch, gold):
+    x = dev(torch, gold["a4/x"])
+    for qt in range(4):
+        for tag, (s, z) in {"p0": (1.0, 0), "p1": (0.37, 3)}.items():
+            qz = dllm.DefaultQuantizer(8, True, None, scale=s, zero_point=z)
+            t = qz.quantize(x, dllm.QuantizationType(qt))
+            assert np.array_equal(host(t.data), gold[f"a4/qt{qt}/{tag}/q"].ravel()), (qt, tag)
+            assert same_bits(host(qz.dequantize(t)).ravel(), gold[f"a4/qt{qt}/{tag}/deq"])
+            assert tuple(t.shape) == (64, 64)
+
+
+def test_quant_utils_int8_1024sq(dllm, torch, orc):
+    """Config 1: int8 symmetric quantize -> dequantize round trip on 1024x1024 N(0,1) (bit-exact)."""
+    x = np.random.default_rng(0).standard_normal((1024, 1024)).astype(np.float32)
+    t = dllm.quant_utils.quantize(dev(torch, x), dllm.QuantizationType.Int8, True, None)
+    y = dllm.quant_utils.dequantize(t)
+    q = orc.default_quantize(x, 0, 1.0, 0)
+    assert np.array_equal(host(t.data), q)
+    assert same_bits(host(y).ravel(), orc.default_dequantize(q, 1.0, 0))
+
+
+# ---- a8 -----------------------------------------------------------------------------------------
+
+def test_bit_quantizer_golden(dllm, torch, gold):
+    x = dev(torch, gold["a8/x"])
+    for bits in (2, 4, 8, 16):
+        for tag in ("pref", "aff"):
+            s, z = gold[f"a8/b{bits}/{tag}/params"]
+            bq = dllm.BitQuantizer(float(s), float(z))
+            q = bq.quantize(x, bits)
+            assert np.array_equal(host(q), gold[f"a8/b{bits}/{tag}/q"]), (bits, tag)
+            assert same_bits(host(bq.dequantize(q, bits)), gold[f"a8/b{bits}/{tag}/deq"])
+
+
+def test_compress_vectors_golden(dllm, torch, gold):
+    for bits in (2, 4, 8, 16):
+        q, s, z = dllm.compress_vectors(dev(torch, gold[f"a8iii/b{bits}/x"]), bits)
+        assert np.array_equal(host(q), gold[f"a8iii/b{bits}/q"])
+        assert same_bits(host(s), gold[f"a8iii/b{bits}/scale"]) and same_bits(host(z), gold[f"a8iii/b{bits}/zp"])
+        y = dllm.decompress_vectors(q, s, z)
+        exp = np.stack([np.asarray((gold[f"a8iii/b{bits}/q"][i].astype(np.float32) * gold[f"a8iii/b{bits}/scale"][i])
+                                   .astype(np.float32) + gold[f"a8iii/b{bits}/zp"][i], np.float32)
+                        for i in range(q.shape[0])])
+        assert same_bits(host(y), exp)
+
+
+def test_prefill_kvquant_quantize_vectors(dllm, torch, gold, orc):
+    pk = dllm.PrefillKVQuant(dllm.SystemConfig())
+    q, w = pk.quantize_vectors_batched(dev(torch, gold["qv/x"]), [2, 4])
+    assert np.array_equal(host(q), gold["qv/q"]) and np.array_equal(w, gold["qv/widths"])
+    # long cycle (> 64 slots) and many rows
+    rng = np.random.default_rng(5)
+    x = rng.uniform(-0.5, 1.5, (300, 40)).astype(np.float32)
+    req = rng.choice([0, 1, 2, 3, 4, 5, 6, 7], 70).astype(np.uint8)
+    q, w = pk.quantize_vectors_batched(dev(torch, x), req)
+    rq, rw = orc.quantize_vectors(x, [4, 6, 8, 16], req)
+    assert np.array_equal(host(q), rq) and np.array_equal(w, rw)
+    with pytest.raises(dllm.InvalidParams):
+        pk.quantize_vectors_batched(dev(torch, x), [8])
+
+
+# ---- a10 ----------------------------------------------------------------------------------------
+
+def test_calibration_golden(dllm, torch, gold):
+    cal = dllm.CalibrationData.new(64, False)
+    for i in range(3):
+        cal.update(dev(torch, gold[f"a10/rand/x{i}"]))
+    assert same_bits(np.array([cal.min, cal.max], np.float32), gold["a10/rand/minmax"])
+    assert np.array_equal(host(cal.histogram), gold["a10/rand/hist"])
+    for bits in (4, 8):
+        for sym in (0, 1):
+            p = cal.compute_params(bits, bool(sym))
+            exp = gold[f"a10/rand/params_b{bits}_s{sym}"]
+            assert np.float32(p.scale) == exp[0] and p.zero_point == int(exp[1])
+    ref = dllm.CalibrationData.new(10, False)
+    ref.update(dev(torch, np.array([[1, 2, 3], [4, 5, 6]], np.float32)))
+    assert np.array_equal(host(ref.histogram), gold["a10/ref/hist"])
+    with pytest.raises(dllm.CalibrationRequired):
+        dllm.CalibrationData.new(4, False).compute_params(8, False)
+
+
+# ---- a5: group-quantized linear -----------------------------------------------------------------
+
+def _linear_case(dllm, torch, orc, M, K, N, bits, ydt, seed=0, bias=True):
+    rng = np.random.default_rng(seed)
+    W = (0.02 * rng.standard_normal((K, N))).astype(np.float32)
+    X = rng.standard_normal((M, K)).astype(np.float32)
+    b = (0.1 * rng.standard_normal(N)).astype(np.float32) if bias else None
+    lin = dllm.QuantLinear.from_weight(dev(torch, W), None if b is None else dev(torch, b), bits, 128)
+    codes, scales, zps = orc.quantize_weights(W, bits, 128)
+    pc, ps, pz = lin.export()
+    assert np.array_equal(host(pc), orc.pack_bits(codes.ravel(), bits)), "weight codes differ"
+    assert same_bits(host(ps), scales) and np.array_equal(host(pz), zps), "weight scales/zps differ"
+    Y = lin(dev(torch, X).half(), out_dtype=ydt)
+    Yr = orc.linear_forward(X, orc.dequantize_weights(codes, scales, zps, 128), b, nthreads=8)
+    return host(Y.float()), Yr, lin, X
+
+
+@pytest.mark.parametrize("M,K,N", [(16, 256, 96), (64, 512, 256), (256, 1024, 512), (300, 640, 200),
+                                   (1, 128, 128), (513, 256, 384)])
+def test_linear_int4_shapes(dllm, torch, orc, M, K, N):
+    for ydt in (torch.float32, torch.float16):
+        Y, Yr, _, _ = _linear_case(dllm, torch, orc, M, K, N, 4, ydt)
+        assert rel_err(Y, Yr) <= REL_TOL, (M, K, N, ydt, rel_err(Y, Yr))
+
+
+@pytest.mark.parametrize("bits", [2, 8])
+def test_linear_other_widths(dllm, torch, orc, bits):
+    Y, Yr, _, _ = _linear_case(dllm, torch, orc, 128, 512, 256, bits, torch.float32, seed=bits)
+    assert rel_err(Y, Yr) <= REL_TOL, rel_err(Y, Yr)
+
+
+def test_linear_exact_integer_layout(dllm, torch, orc):
+    """Asymmetric exact-integer data: catches any row/col swap in the MFMA fragment maps.
+    W columns use 16 distinct levels exactly (scale 1, zp 0 per group), X small integers, so
+    the f16 GEMM is exact and must equal the f64 product bit for bit."""
+    K, N, M = 256, 128, 64
+    rng = np.random.default_rng(9)
+    W = rng.integers(0, 16, (K, N)).astype(np.float32)
+    W[0, :], W[1, :] = 0.0, 15.0  # pin min/max of group 0 -> scale 1, zp 0
+    W[128, :], W[129, :] = 0.0, 15.0
+    X = rng.integers(-3, 4, (M, K)).astype(np.float32)
+    lin = dllm.QuantLinear.from_weight(dev(torch, W), None, 4, 128)
+    Y = host(lin(dev(torch, X).half(), out_dtype=torch.float32))
+    assert np.array_equal(Y, (X.astype(np.float64) @ W.astype(np.float64)).astype(np.float32))
+
+
+def test_linear_from_quantized_roundtrip(dllm, torch, orc):
+    rng = np.random.default_rng(4)
+    K, N = 512, 256
+    W = (0.02 * rng.standard_normal((K, N))).astype(np.float32)
+    codes, scales, zps = orc.quantize_weights(W, 4, 128)
+    lin = dllm.QuantLinear.from_quantized(dev(torch, orc.pack_bits(codes.ravel(), 4)), dev(torch, scales),
+                                          dev(torch, zps), K, N, 4, 128)
+    X = rng.standard_normal((32, K)).astype(np.float32)
+    Y = host(lin(dev(torch, X), out_dtype=torch.float32))  # f32 X path (cast kernel)
+    Yr = orc.linear_forward(X, orc.dequantize_weights(codes, scales, zps, 128))
+    assert rel_err(Y, Yr) <= REL_TOL
+    lin2 = dllm.QuantLinear.from_weight(dev(torch, W), None, 4, 128)
+    Y2 = host(lin2(dev(torch, X), out_dtype=torch.float32))
+    assert np.array_equal(Y, Y2), "import path and quantize path disagree"
+
+
+def test_linear_full_size_vs_torch_fp32(dllm, torch, orc):
+    """Config 2 / metric shape (M=4096, K=N=4096): the f32 reference product of the oracle's
+    dequantized weights, computed by torch fp32 on the GPU (no TF32 on gfx950)."""
+    M = K = N = 4096
+    g = torch.Generator(device="cuda").manual_seed(2)
+    W = 0.02 * torch.randn(K, N, device="cuda", generator=g)
+    X = torch.randn(M, K, device="cuda", generator=g).half()
+    lin = dllm.QuantLinear.from_weight(W, None, 4, 128)
+    Y = lin(X, out_dtype=torch.float16).float()
+    codes, scales, zps = orc.quantize_weights(host(W), 4, 128)
+    pc, ps, pz = lin.export()
+    assert np.array_equal(host(pc), orc.pack_bits(codes.ravel(), 4)) and same_bits(host(ps), scales)
+    Wh = dev(torch, orc.dequantize_weights(codes, scales, zps, 128))
+    Yr = X.float() @ Wh
+    rel = (torch.linalg.norm(Y - Yr) / torch.linalg.norm(Yr)).item()
+    assert rel <= REL_TOL, rel
+
+
+def test_mixed_precision_stack(dllm, torch, orc):
+    """Config 3 shape family: layers cycle bits [2, 4]; each layer within tolerance of the f32
+    restatement applied to the same f16 input."""
+    rng = np.random.default_rng(12)
+    d, M, L = 512, 96, 4
+    Ws = [(0.05 * rng.standard_normal((d, d))).astype(np.float32) for _ in range(L)]
+    stack = dllm.MixedPrecisionStack([dev(torch, w) for w in Ws], bits=(2, 4))
+    x = dev(torch, rng.standard_normal((M, d)).astype(np.float32)).half()
+    h = x
+    for i, layer in enumerate(stack.layers):
+        assert layer.bits == (2, 4)[i % 2]
+        y = layer(h, out_dtype=torch.float16)
+        c, s, z = orc.quantize_weights(Ws[i], layer.bits, 128)
+        yr = orc.linear_forward(host(h.float()), orc.dequantize_weights(c, s, z, 128))
+        assert rel_err(host(y.float()), yr) <= REL_TOL, (i, rel_err(host(y.float()), yr))
+        h = y
+    assert torch.equal(stack(x), h)
