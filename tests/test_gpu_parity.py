@@ -108,7 +108,7 @@ def test_quantized_kv_cache_entry(dllm, torch, orc):
         rq, rs, rz = orc.quantize_tensor(ref, 4)
         assert same_bits(host(t).ravel(), orc.dequantize_tensor(rq, rs, rz))
     assert e.keys.compression_ratio() == pytest.approx(8.0)
-    assert e.memory_usage() == 2 * (K.size * 4 + 7) // 8
+    assert e.memory_usage() == 2 * ((K.size * 4 + 7) // 8)
 
 
 # ---- a4 -----------------------------------------------------------------------------------------
