@@ -93,6 +93,7 @@ SIGNATURES = {
     "dllm_linear_export": (INT, [P, P, P, P, P]),
     "dllm_linear_info": (INT, [P, P, P, P, P]),
     "dllm_linear_weight_bytes": (S, [P]),
+    "dllm_linear_set_kernel_variant": (INT, [P, INT]),
     "dllm_linear_destroy": (INT, [P]),
     "dllm_kv_attention": (INT, [P, P, P, P, P, U8, S, S, S, P, P]),
 }

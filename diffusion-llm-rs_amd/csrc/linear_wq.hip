@@ -33,7 +33,8 @@ struct dllm_linear {
     size_t K = 0, N = 0, Npad = 0, G = 0, group = 0;
     int bits = 0;
     int device = 0;
-    uint32_t *wdev = nullptr;     // fragment-major words
+    uint32_t *wdev = nullptr;     // prefill layout (32x32x16 fragments)
+    uint32_t *wdec = nullptr;     // decode layout (16x16x32 fragments)
     uint32_t *sz = nullptr;       // [G][Npad]
     uint32_t *canon = nullptr;    // canonical packed codes (u32-padded)
     float *scales = nullptr;      // [G][N]
@@ -41,6 +42,7 @@ struct dllm_linear {
     float *bias = nullptr;        // [Npad]
     __half *xws = nullptr;        // f32 -> f16 staging for X
     size_t xws_elems = 0;
+    int variant = 3;              // prefill schedule variant (tuning knob, see wq_gemm_kernel)
     std::mutex mu;
 };
 
@@ -116,6 +118,31 @@ __global__ void __launch_bounds__(256) build_fragments_kernel(const uint32_t *__
     }
 }
 
+// Canonical -> decode layout.  One thread per (column n < Npad, 128-deep slab).
+__global__ void __launch_bounds__(256) build_decode_kernel(const uint32_t *__restrict__ canon, size_t K, size_t N,
+                                                           size_t Npad, int bits, uint32_t *__restrict__ wdec) {
+    const size_t n = blockIdx.x * static_cast<size_t>(256) + threadIdx.x;
+    const size_t slab = blockIdx.y;
+    if (n >= Npad) return;
+    const size_t nslab = (K + 127) / 128, nt = n >> 4;
+    const int pairs_per_word = 16 / bits;
+    for (int o = 0; o < 4; ++o) {
+        const size_t lane = (n & 15) + 16 * o;
+        uint32_t *dst = wdec + ((nt * nslab + slab) * 64 + lane) * bits;
+        for (int w = 0; w < bits; ++w) {
+            uint32_t word = 0;
+            for (int p = 0; p < pairs_per_word; ++p) {
+                const int P = w * pairs_per_word + p, t = P >> 2, v = P & 3;
+                const size_t k = slab * 128 + t * 32 + 8 * o + 2 * v;
+                uint32_t lo = 0, hi = 0;
+                if (n < N && k < K) { lo = canon_code(canon, k, n, N, bits); hi = canon_code(canon, k + 1, n, N, bits); }
+                word |= (lo << (bits * p)) | (hi << (16 + bits * p));
+            }
+            dst[w] = word;
+        }
+    }
+}
+
 __global__ void __launch_bounds__(256) build_sz_kernel(const float *__restrict__ scales, const uint8_t *__restrict__ zps,
                                                        size_t G, size_t N, size_t Npad, uint32_t *__restrict__ sz) {
     const size_t n = blockIdx.x * static_cast<size_t>(256) + threadIdx.x;
@@ -145,40 +172,34 @@ __global__ void __launch_bounds__(256) cast_f32_f16_kernel(const float *__restri
 }
 
 // ---------------------------------------------------------------------------------------------
-// GEMM: Y[M][N] = X[M][K] (f16) . W^[K][N] + b, computed as Y^T = W^^T X^T so that the
-// accumulator's lane index is the token m and 4 consecutive registers hold 4 consecutive
-// output columns n (one 8/16-byte store each).
-//   block tile 256 (m) x 128 (n), 4 waves as 2 (m) x 2 (n), wave tile 128 x 64:
-//   acc[2 n-reps][4 m-reps] of 32x32 f32 = 128 VGPRs.
-//   X tile [256][64] f16 in LDS (2 buffers, 64 KiB), filled by global_load_lds 16 B/lane with
-//   the 16-B chunk index XOR-swizzled by (row>>1)&7 (conflict-free ds_read_b128 fragments).
-//   W fragments stream straight to VGPRs (one coalesced dwordx4 per lane per slab for int4)
-//   one slab ahead, and are dequantized in registers (4 VALU per 2 weights).
+// Prefill GEMM (M > decode threshold): Y[M][N] = X[M][K] (f16) . W^[K][N] + b, computed as
+// Y^T = W^^T X^T so that the accumulator's lane index is the token m and 4 consecutive
+// registers hold 4 consecutive output columns n (one 8/16-byte store each).
+//   block tile 256 (m) x 128 (n), 4 waves side by side in n, wave tile 256 (m) x 32 (n):
+//   acc[8 m-reps] of 32x32 f32 = 128 VGPRs.  Each wave dequantizes only its own 32 columns
+//   (no redundant dequant; 2.5 VALU per MFMA) and all 4 waves share the X tile.
+//   X tile [256][64] f16 in LDS (2 stages, 64 KiB -> 2 blocks per CU), filled by
+//   global_load_lds 16 B/lane with the 16-B chunk index XOR-swizzled by (row>>1)&7
+//   (conflict-free ds_read_b128 fragments, measured SQ_LDS_BANK_CONFLICT = 0).
+//   W fragments stream straight to VGPRs, one coalesced dwordx4 per lane per 64-deep slab
+//   (int4), one slab ahead.
 // ---------------------------------------------------------------------------------------------
 template <int BITS>
-struct WSlab { uint32_t w[2][BITS]; };
-
-template <int BITS>
-__device__ __forceinline__ void load_wslab(WSlab<BITS> &ws, const uint32_t *__restrict__ wdev, size_t nk,
-                                           size_t nt0, size_t kt, int lane) {
-#pragma unroll
-    for (int rep = 0; rep < 2; ++rep) {
-        const uint32_t *p = wdev + (((nt0 + rep) * nk + kt) * 64 + lane) * BITS;
-        if constexpr (BITS == 4) {
-            uint4 v = *reinterpret_cast<const uint4 *>(p);
-            ws.w[rep][0] = v.x; ws.w[rep][1] = v.y; ws.w[rep][2] = v.z; ws.w[rep][3] = v.w;
-        } else if constexpr (BITS == 2) {
-            uint2 v = *reinterpret_cast<const uint2 *>(p);
-            ws.w[rep][0] = v.x; ws.w[rep][1] = v.y;
-        } else {
-            uint4 a = *reinterpret_cast<const uint4 *>(p), b = *reinterpret_cast<const uint4 *>(p + 4);
-            ws.w[rep][0] = a.x; ws.w[rep][1] = a.y; ws.w[rep][2] = a.z; ws.w[rep][3] = a.w;
-            ws.w[rep][4] = b.x; ws.w[rep][5] = b.y; ws.w[rep][6] = b.z; ws.w[rep][7] = b.w;
-        }
+__device__ __forceinline__ void load_words(uint32_t (&w)[BITS], const uint32_t *__restrict__ p) {
+    if constexpr (BITS == 4) {
+        uint4 v = *reinterpret_cast<const uint4 *>(p);
+        w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+    } else if constexpr (BITS == 2) {
+        uint2 v = *reinterpret_cast<const uint2 *>(p);
+        w[0] = v.x; w[1] = v.y;
+    } else {
+        uint4 a = *reinterpret_cast<const uint4 *>(p), b = *reinterpret_cast<const uint4 *>(p + 4);
+        w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+        w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
     }
 }
 
-// Dequantizes the A fragment (8 f16) of substep s from the slab words.
+// Dequantizes the A fragment (8 f16) of substep s from a lane's slab words.
 template <int BITS>
 __device__ __forceinline__ half8_t dequant_frag(const uint32_t (&w)[BITS], int s, half2_t nz, half2_t sc) {
     constexpr int PPW = 16 / BITS;
@@ -196,6 +217,12 @@ __device__ __forceinline__ half8_t dequant_frag(const uint32_t (&w)[BITS], int s
         r[2 * v + 1] = h[1];
     }
     return r;
+}
+
+__device__ __forceinline__ void split_sz(uint32_t szv, half2_t &nz, half2_t &sc) {
+    half2_t p = __builtin_bit_cast(half2_t, szv);
+    nz = half2_t{p[0], p[0]};
+    sc = half2_t{p[1], p[1]};
 }
 
 __device__ __forceinline__ void glds16(const void *gsrc, void *ldst) {
@@ -222,12 +249,78 @@ __device__ __forceinline__ void store1<float>(float *p, float a) { *p = a; }
 template <>
 __device__ __forceinline__ void store1<__half>(__half *p, float a) { *p = __float2half_rn(a); }
 
-template <int BITS, typename YT>
+// Stores 4 consecutive outputs y[n..n+3] (+ bias), masking n >= N.
+template <typename YT>
+__device__ __forceinline__ void store_out4(YT *yrow, const float *__restrict__ bias, int n, int N, bool vec_ok,
+                                           float a0, float a1, float a2, float a3) {
+    if (n >= N) return;
+    const float4 bv = *reinterpret_cast<const float4 *>(bias + n);
+    const float y0 = a0 + bv.x, y1 = a1 + bv.y, y2 = a2 + bv.z, y3 = a3 + bv.w;
+    if (vec_ok) {
+        store4<YT>(yrow + n, y0, y1, y2, y3);
+    } else {
+        store1<YT>(yrow + n, y0);
+        if (n + 1 < N) store1<YT>(yrow + n + 1, y1);
+        if (n + 2 < N) store1<YT>(yrow + n + 2, y2);
+        if (n + 3 < N) store1<YT>(yrow + n + 3, y3);
+    }
+}
+
+constexpr int kMReps = kBM / 32;   // 8
+
+// LDS stage layout (bytes): X tile [256][64] f16 (32 KiB) | W slabs [4 waves][64 lanes][BITS words]
+// | sz [4 waves][64 lanes] u32.  Everything arrives by global_load_lds, so hipcc's counters see no
+// register-destination global load in the loop (mixing the two kinds makes it wait vmcnt(0) at
+// the first use of a register load, which serialised prefetch and compute in the first version).
+template <int BITS>
+struct StageLayout {
+    static constexpr int kX = kBM * kBK * 2;
+    static constexpr int kW = 4 * 64 * BITS * 4;
+    static constexpr int kSZ = 4 * 64 * 4;
+    static constexpr int kBytes = kX + kW + kSZ;
+};
+
+template <int BITS>
+__device__ __forceinline__ void glds_words(const uint32_t *gsrc, uint8_t *ldst) {
+    // One lane-linear LDS-DMA of BITS*4 bytes per lane (16 B for int4; 8 B as two dwords for int2).
+    if constexpr (BITS == 4) {
+        glds16(gsrc, ldst);
+    } else if constexpr (BITS == 8) {
+        glds16(gsrc, ldst);
+        glds16(gsrc + 4, ldst + 64 * 16);
+    } else {
+        __builtin_amdgcn_global_load_lds((gbl_void_ptr)(const_cast<uint32_t *>(gsrc)), (lds_void_ptr)(ldst), 4, 0, 0);
+        __builtin_amdgcn_global_load_lds((gbl_void_ptr)(const_cast<uint32_t *>(gsrc + 1)), (lds_void_ptr)(ldst + 256),
+                                         4, 0, 0);
+    }
+}
+
+template <int BITS>
+__device__ __forceinline__ void lds_words(uint32_t (&w)[BITS], const uint8_t *wbase, int lane) {
+    if constexpr (BITS == 4) {
+        uint4 v = *reinterpret_cast<const uint4 *>(wbase + lane * 16);
+        w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+    } else if constexpr (BITS == 8) {
+        uint4 a = *reinterpret_cast<const uint4 *>(wbase + lane * 16);
+        uint4 b = *reinterpret_cast<const uint4 *>(wbase + 64 * 16 + lane * 16);
+        w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+    } else {
+        w[0] = *reinterpret_cast<const uint32_t *>(wbase + lane * 4);
+        w[1] = *reinterpret_cast<const uint32_t *>(wbase + 256 + lane * 4);
+    }
+}
+
+template <int BITS, typename YT, int VAR>
 __global__ void __launch_bounds__(kThreads, 2)
 wq_gemm_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdev,
                const uint32_t *__restrict__ sz, const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad,
                int group, int nbm, int nbn) {
-    __shared__ __attribute__((aligned(16))) _Float16 xs[2 * kBM * kBK];   // the ONE LDS array
+    using SL = StageLayout<BITS>;
+    // Two stage arrays (not one array indexed at run time): with distinct objects the compiler
+    // can prove the LDS-DMA into one stage does not alias the ds_reads of the other, and does not
+    // insert a vmcnt(0) before every fragment read.
+    __shared__ __attribute__((aligned(16))) uint8_t smem0[SL::kBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t smem1[SL::kBytes];
 
     // XCD-aware bijective remap: consecutive logical tiles (same bm row panel of X) share an XCD.
     const int nb = nbm * nbn, orig = blockIdx.x;
@@ -236,12 +329,13 @@ wq_gemm_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__res
     const int bm = wgid / nbn, bn = wgid % nbn;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave >> 1, wn = wave & 1;
     const int m0 = bm * kBM, n0 = bn * kBN;
-    const size_t nk = static_cast<size_t>(K) / kBK;
-    const size_t nt0 = static_cast<size_t>(n0 + wn * 64) >> 5;
+    const unsigned nk = static_cast<unsigned>(K) / kBK;
+    const unsigned kpg = static_cast<unsigned>(group) / kBK;   // k-steps per quantization group
+    const unsigned nt = static_cast<unsigned>(n0 + wave * 32) >> 5;
+    const int ncol = n0 + wave * 32 + (lane & 31);
 
-    // glds source rows for this thread (8 instructions x 32 rows per buffer).
+    // glds source pointers.
     const int chunk_st = lane & 7;
     const __half *xsrc[8];
 #pragma unroll
@@ -252,127 +346,258 @@ wq_gemm_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__res
         const int c = chunk_st ^ ((row >> 1) & 7);
         xsrc[i] = X + static_cast<size_t>(grow) * K + c * 8;
     }
-    auto stage_x = [&](int buf, size_t kt) {
-        _Float16 *base = xs + buf * (kBM * kBK) + wave * 512;   // 1 KiB per wave-instruction
+    const uint32_t *wsrc = wdev + (static_cast<size_t>(nt) * nk * 64 + lane) * BITS;   // + kt*64*BITS
+    const uint32_t *szsrc = sz + ncol;                                                  // + g*Npad
+
+    auto stage = [&](uint8_t *sb, unsigned kt) {
+        uint8_t *xb = sb + wave * 1024;   // 1 KiB per wave-instruction
 #pragma unroll
-        for (int i = 0; i < 8; ++i) glds16(xsrc[i] + kt * kBK, base + i * 2048);
+        for (int i = 0; i < 8; ++i) glds16(xsrc[i] + kt * kBK, xb + i * 4096);
+        glds_words<BITS>(wsrc + static_cast<size_t>(kt) * 64 * BITS, sb + SL::kX + wave * (64 * BITS * 4));
+        __builtin_amdgcn_global_load_lds((gbl_void_ptr)(const_cast<uint32_t *>(szsrc + (kt / kpg) * Npad)),
+                                         (lds_void_ptr)(sb + SL::kX + SL::kW + wave * 256), 4, 0, 0);
     };
 
-    float16_t acc[2][4];
+    float16_t acc[kMReps];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int r = 0; r < kMReps; ++r)
 #pragma unroll
-        for (int b = 0; b < 4; ++b)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
+        for (int e = 0; e < 16; ++e) acc[r][e] = 0.0f;
 
-    auto load_sz = [&](size_t kt, uint32_t (&out)[2]) {
-        const size_t g = (kt * kBK) / group;
-#pragma unroll
-        for (int rep = 0; rep < 2; ++rep) out[rep] = sz[g * Npad + n0 + wn * 64 + rep * 32 + (lane & 31)];
-    };
-
-    WSlab<BITS> wcur, wnxt;
-    uint32_t szc[2], szn[2];
-    stage_x(0, 0);
-    load_wslab<BITS>(wcur, wdev, nk, nt0, 0, lane);
-    load_sz(0, szc);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-
-    // LDS fragment read offsets (in halves) for the 4 m-reps; chunk = 2*s + (lane>>5).
-    int rowoff[4], rowx[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int row = wm * 128 + r * 32 + (lane & 31);
-        rowoff[r] = row * kBK;
-        rowx[r] = (row >> 1) & 7;
-    }
+    // LDS fragment offsets (bytes): row = 32r + (lane&31); (row>>1)&7 does not depend on r.
     const int hsel = lane >> 5;
+    const int rowx = ((lane & 31) >> 1) & 7;
+    int soff[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) soff[s] = (lane & 31) * (kBK * 2) + ((((2 * s + hsel) ^ rowx)) << 4);
 
-    for (size_t kt = 0; kt < nk; ++kt) {
-        const int cur = static_cast<int>(kt & 1);
-        if (kt + 1 < nk) {
-            stage_x(cur ^ 1, kt + 1);
-            load_wslab<BITS>(wnxt, wdev, nk, nt0, kt + 1, lane);
-            load_sz(kt + 1, szn);
-        }
-        half2_t nz[2], sc[2];
+    // One 64-deep k-step on stage `sb` while stage `nb_` fills with k-step kt+1.
+    // One 64-deep k-step on stage `sb` while stage `nb_` fills with k-step kt+1.
+    // VAR 0: fragment reads / dequant+MFMA in sched_barrier-fenced blocks (reads one substep ahead);
+    // VAR 1: same data flow, compiler-scheduled; VAR 2: A and B fragments both one substep ahead,
+    // MFMAs interleaved with the next substep's ds_reads and dequant VALU by sched_group_barrier;
+    // VAR 3: VAR 2 + s_setprio(1) around each MFMA group.
+    auto read_b = [&](half8_t (&b)[kMReps], const uint8_t *sb, int s) {
 #pragma unroll
-        for (int rep = 0; rep < 2; ++rep) {
-            half2_t p = __builtin_bit_cast(half2_t, szc[rep]);
-            nz[rep] = half2_t{p[0], p[0]};
-            sc[rep] = half2_t{p[1], p[1]};
-        }
-        const _Float16 *xb = xs + cur * (kBM * kBK);
+        for (int r = 0; r < kMReps; ++r) b[r] = *reinterpret_cast<const half8_t *>(sb + soff[s] + r * 32 * kBK * 2);
+    };
+    auto mfma8 = [&](const half8_t &a, const half8_t (&b)[kMReps]) {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            half8_t a0 = dequant_frag<BITS>(wcur.w[0], s, nz[0], sc[0]);
-            half8_t a1 = dequant_frag<BITS>(wcur.w[1], s, nz[1], sc[1]);
-            const int chunk = 2 * s + hsel;
+        for (int r = 0; r < kMReps; ++r) acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b[r], acc[r], 0, 0, 0);
+    };
+    auto step = [&](const uint8_t *sb, uint8_t *nb_, unsigned kt) {
+        if (kt + 1 < nk) stage(nb_, kt + 1);
+        uint32_t w[BITS];
+        lds_words<BITS>(w, sb + SL::kX + wave * (64 * BITS * 4), lane);
+        half2_t nz, sc;
+        split_sz(*reinterpret_cast<const uint32_t *>(sb + SL::kX + SL::kW + wave * 256 + lane * 4), nz, sc);
+        half8_t bA[kMReps], bB[kMReps];
+        read_b(bA, sb, 0);
+        if constexpr (VAR <= 1) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const half8_t b = *reinterpret_cast<const half8_t *>(xb + rowoff[r] + ((chunk ^ rowx[r]) << 3));
-                acc[0][r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b, acc[0][r], 0, 0, 0);
-                acc[1][r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b, acc[1][r], 0, 0, 0);
+            for (int s = 0; s < 4; s += 2) {
+                read_b(bB, sb, s + 1);
+                if constexpr (VAR == 0) __builtin_amdgcn_sched_barrier(0);
+                mfma8(dequant_frag<BITS>(w, s, nz, sc), bA);
+                if constexpr (VAR == 0) __builtin_amdgcn_sched_barrier(0);
+                if (s + 2 < 4) read_b(bA, sb, s + 2);
+                if constexpr (VAR == 0) __builtin_amdgcn_sched_barrier(0);
+                mfma8(dequant_frag<BITS>(w, s + 1, nz, sc), bB);
+                if constexpr (VAR == 0) __builtin_amdgcn_sched_barrier(0);
             }
+        } else {
+            half8_t aA = dequant_frag<BITS>(w, 0, nz, sc), aB;
+            auto sub = [&](half8_t (&bc)[kMReps], half8_t (&bn)[kMReps], const half8_t &ac, half8_t &an, int s) {
+                __builtin_amdgcn_sched_barrier(0);
+                if constexpr (VAR == 3) __builtin_amdgcn_s_setprio(1);
+                if (s < 3) {
+                    read_b(bn, sb, s + 1);
+                    an = dequant_frag<BITS>(w, s + 1, nz, sc);
+                }
+                mfma8(ac, bc);
+#pragma unroll
+                for (int i = 0; i < kMReps; ++i) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+                    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);   // VALU
+                }
+                if constexpr (VAR == 3) __builtin_amdgcn_s_setprio(0);
+                __builtin_amdgcn_sched_barrier(0);
+            };
+            sub(bA, bB, aA, aB, 0);
+            sub(bB, bA, aB, aA, 1);
+            sub(bA, bB, aA, aB, 2);
+            sub(bB, bA, aB, aA, 3);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (kt + 1 < nk) {
-            wcur = wnxt;
-            szc[0] = szn[0]; szc[1] = szn[1];
-        }
+    };
+
+    stage(smem0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (unsigned kt = 0; kt < nk; kt += 2) {
+        step(smem0, smem1, kt);
+        if (kt + 1 < nk) step(smem1, smem0, kt + 1);
     }
 
-    // Epilogue: acc[rep][r] reg e -> n = nbase + (e&3) + 8*(e>>2) + 4*(lane>>5), m = mbase + (lane&31).
-    const bool vec_ok = (N % 4) == 0;
+    // Epilogue: acc[r] reg e -> n = n0 + 32*wave + (e&3) + 8*(e>>2) + 4*hsel, m = m0 + 32r + (lane&31).
+    const int nb0 = n0 + wave * 32 + 4 * hsel;
+    float4 bv[4];
 #pragma unroll
-    for (int rep = 0; rep < 2; ++rep) {
+    for (int qd = 0; qd < 4; ++qd) bv[qd] = *reinterpret_cast<const float4 *>(bias + nb0 + 8 * qd);
+    const bool full = (m0 + kBM <= M) && (n0 + kBN <= N) && (N % 4) == 0;
+    if (full) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int m = m0 + wm * 128 + r * 32 + (lane & 31);
+        for (int r = 0; r < kMReps; ++r) {
+            YT *yrow = Y + static_cast<size_t>(m0 + r * 32 + (lane & 31)) * N + nb0;
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd)
+                store4<YT>(yrow + 8 * qd, acc[r][4 * qd + 0] + bv[qd].x, acc[r][4 * qd + 1] + bv[qd].y,
+                           acc[r][4 * qd + 2] + bv[qd].z, acc[r][4 * qd + 3] + bv[qd].w);
+        }
+    } else {
+        const bool vec_ok = (N % 4) == 0;
+#pragma unroll
+        for (int r = 0; r < kMReps; ++r) {
+            const int m = m0 + r * 32 + (lane & 31);
             if (m >= M) continue;
             YT *yrow = Y + static_cast<size_t>(m) * N;
 #pragma unroll
-            for (int qd = 0; qd < 4; ++qd) {
-                const int n = n0 + wn * 64 + rep * 32 + 8 * qd + 4 * hsel;
-                if (n >= N) continue;
-                const float4 bv = *reinterpret_cast<const float4 *>(bias + n);
-                const float y0 = acc[rep][r][4 * qd + 0] + bv.x, y1 = acc[rep][r][4 * qd + 1] + bv.y;
-                const float y2 = acc[rep][r][4 * qd + 2] + bv.z, y3 = acc[rep][r][4 * qd + 3] + bv.w;
-                if (vec_ok) {
-                    store4<YT>(yrow + n, y0, y1, y2, y3);
-                } else {
-                    store1<YT>(yrow + n, y0);
-                    if (n + 1 < N) store1<YT>(yrow + n + 1, y1);
-                    if (n + 2 < N) store1<YT>(yrow + n + 2, y2);
-                    if (n + 3 < N) store1<YT>(yrow + n + 3, y3);
+            for (int qd = 0; qd < 4; ++qd)
+                store_out4<YT>(yrow, bias, nb0 + 8 * qd, N, vec_ok, acc[r][4 * qd + 0], acc[r][4 * qd + 1],
+                               acc[r][4 * qd + 2], acc[r][4 * qd + 3]);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Decode GEMM (small M, weight-streaming / HBM-bound): one block per 16-column n-tile
+// (N/16 blocks = 256 at N = 4096, one per CU), 8 waves split K by 128-deep slabs, 16x16x32
+// f16 MFMA with the weight as A (16 columns) and MT 16-token tiles of X as B, then the 8 wave
+// partials are summed through LDS (no cross-block reduction, deterministic order).
+// Decode layout: [n16 tile][k128 slab][lane][BITS words], lane l = (n & 15) + 16 * ((k % 32) / 8),
+// word/pair order as the prefill layout with the 32-deep step t in place of the substep.
+// ---------------------------------------------------------------------------------------------
+typedef float float4_t __attribute__((ext_vector_type(4)));
+constexpr int kDecWaves = 8;
+
+template <int BITS, typename YT, int MT>
+__global__ void __launch_bounds__(kDecWaves * 64)
+wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdec,
+                 const uint32_t *__restrict__ sz, const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad,
+                 int group) {
+    __shared__ __attribute__((aligned(16))) float red[kDecWaves * MT * 64 * 4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n0 = blockIdx.x * 16;
+    const int nslab = (K + 127) / 128;
+    const int ncol = n0 + (lane & 15);
+    const int ko = 8 * (lane >> 4);
+    const uint32_t *wbase = wdec + (static_cast<size_t>(blockIdx.x) * nslab * 64 + lane) * BITS;
+
+    const __half *xrow[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        int m = mt * 16 + (lane & 15);
+        m = m < M ? m : M - 1;
+        xrow[mt] = X + static_cast<size_t>(m) * K + ko;
+    }
+
+    float4_t acc[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[mt] = float4_t{0.f, 0.f, 0.f, 0.f};
+
+    constexpr int kDepth = 4;   // slabs in flight per wave
+    for (int base = wave; base < nslab; base += kDecWaves * kDepth) {
+        uint32_t w[kDepth][BITS];
+#pragma unroll
+        for (int i = 0; i < kDepth; ++i) {
+            const int slab = base + i * kDecWaves;
+            if (slab < nslab) load_words<BITS>(w[i], wbase + static_cast<size_t>(slab) * 64 * BITS);
+        }
+#pragma unroll
+        for (int i = 0; i < kDepth; ++i) {
+            const int slab = base + i * kDecWaves;
+            if (slab >= nslab) break;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int k = slab * 128 + t * 32;
+                if (k >= K) break;
+                half2_t nz, sc;
+                split_sz(sz[(k / group) * Npad + ncol], nz, sc);
+                const half8_t a = dequant_frag<BITS>(w[i], t, nz, sc);
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt) {
+                    const half8_t b = *reinterpret_cast<const half8_t *>(xrow[mt] + k);
+                    acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, acc[mt], 0, 0, 0);
                 }
             }
         }
     }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+        *reinterpret_cast<float4_t *>(red + ((wave * MT + mt) * 64 + lane) * 4) = acc[mt];
+    __syncthreads();
+    // Wave mt (< MT) sums the 8 partials of m-tile mt in wave order (deterministic).
+    for (int mt = wave; mt < MT; mt += kDecWaves) {
+        float4_t s = float4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int w = 0; w < kDecWaves; ++w) s += *reinterpret_cast<const float4_t *>(red + ((w * MT + mt) * 64 + lane) * 4);
+        const int m = mt * 16 + (lane & 15);
+        if (m < M)
+            store_out4<YT>(Y + static_cast<size_t>(m) * N, bias, n0 + 4 * (lane >> 4), N, (N % 4) == 0, s[0], s[1],
+                           s[2], s[3]);
+    }
 }
 
-template <int BITS>
-int launch_gemm(const dllm_linear *h, const __half *X, size_t M, void *Y, int y_dtype, hipStream_t st) {
-    const int nbm = static_cast<int>((M + kBM - 1) / kBM), nbn = static_cast<int>(h->Npad / kBN);
-    const unsigned nb = static_cast<unsigned>(nbm) * nbn;
-    if (y_dtype == DLLM_F32)
-        wq_gemm_kernel<BITS, float><<<nb, kThreads, 0, st>>>(X, (int)M, (int)h->K, h->wdev, h->sz, h->bias,
-                                                             static_cast<float *>(Y), (int)h->N, (int)h->Npad,
-                                                             (int)h->group, nbm, nbn);
+constexpr int kDecodeMaxM = 64;
+
+template <int BITS, typename YT>
+int launch_decode(const dllm_linear *h, const __half *X, size_t M, YT *Y, hipStream_t st) {
+    const unsigned nb = static_cast<unsigned>(h->Npad / 16);
+    const int Mi = static_cast<int>(M), K = static_cast<int>(h->K), N = static_cast<int>(h->N);
+    const int Np = static_cast<int>(h->Npad), gr = static_cast<int>(h->group);
+    if (M <= 16)
+        wq_decode_kernel<BITS, YT, 1><<<nb, kDecWaves * 64, 0, st>>>(X, Mi, K, h->wdec, h->sz, h->bias, Y, N, Np, gr);
+    else if (M <= 32)
+        wq_decode_kernel<BITS, YT, 2><<<nb, kDecWaves * 64, 0, st>>>(X, Mi, K, h->wdec, h->sz, h->bias, Y, N, Np, gr);
     else
-        wq_gemm_kernel<BITS, __half><<<nb, kThreads, 0, st>>>(X, (int)M, (int)h->K, h->wdev, h->sz, h->bias,
-                                                              static_cast<__half *>(Y), (int)h->N, (int)h->Npad,
-                                                              (int)h->group, nbm, nbn);
+        wq_decode_kernel<BITS, YT, 4><<<nb, kDecWaves * 64, 0, st>>>(X, Mi, K, h->wdec, h->sz, h->bias, Y, N, Np, gr);
     DLLM_LAUNCH_CHECK();
     return DLLM_OK;
 }
 
+template <int BITS, typename YT, int VAR>
+void launch_prefill(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t st) {
+    const int nbm = (M + kBM - 1) / kBM, nbn = static_cast<int>(h->Npad / kBN);
+    const unsigned nb = static_cast<unsigned>(nbm) * nbn;
+    wq_gemm_kernel<BITS, YT, VAR><<<nb, kThreads, 0, st>>>(X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N,
+                                                           (int)h->Npad, (int)h->group, nbm, nbn);
+}
+
+template <int BITS, typename YT>
+int launch_gemm_t(const dllm_linear *h, const __half *X, size_t M, YT *Y, hipStream_t st) {
+    if (M <= static_cast<size_t>(kDecodeMaxM)) return launch_decode<BITS, YT>(h, X, M, Y, st);
+    switch (h->variant) {
+    case 0: launch_prefill<BITS, YT, 0>(h, X, (int)M, Y, st); break;
+    case 1: launch_prefill<BITS, YT, 1>(h, X, (int)M, Y, st); break;
+
+    case 2: launch_prefill<BITS, YT, 2>(h, X, (int)M, Y, st); break;
+    default: launch_prefill<BITS, YT, 3>(h, X, (int)M, Y, st); break;
+    }
+    DLLM_LAUNCH_CHECK();
+    return DLLM_OK;
+}
+
+template <int BITS>
+int launch_gemm(const dllm_linear *h, const __half *X, size_t M, void *Y, int y_dtype, hipStream_t st) {
+    if (y_dtype == DLLM_F32) return launch_gemm_t<BITS, float>(h, X, M, static_cast<float *>(Y), st);
+    return launch_gemm_t<BITS, __half>(h, X, M, static_cast<__half *>(Y), st);
+}
+
 void free_linear(dllm_linear *h) {
     if (!h) return;
-    (void)hipFree(h->wdev); (void)hipFree(h->sz); (void)hipFree(h->canon); (void)hipFree(h->scales);
+    (void)hipFree(h->wdev); (void)hipFree(h->wdec); (void)hipFree(h->sz); (void)hipFree(h->canon); (void)hipFree(h->scales);
     (void)hipFree(h->zps); (void)hipFree(h->bias); (void)hipFree(h->xws);
     delete h;
 }
@@ -397,6 +622,7 @@ int alloc_linear(size_t K, size_t N, uint8_t bits, size_t group, dllm_linear **o
     auto A = [&](void **p, size_t bytes) { return hipMalloc(p, std::max<size_t>(bytes, 16)); };
     hipError_t e = hipSuccess;
     if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->wdev), h->Npad * K * bits / 8);
+    if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->wdec), h->Npad * ((K + 127) / 128) * 128 * bits / 8);
     if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->sz), h->G * h->Npad * 4);
     if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->canon), canon_words(K, N, bits) * 4);
     if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->scales), h->G * N * 4);
@@ -415,6 +641,9 @@ int finish_linear(dllm_linear *h, const float *bias, hipStream_t st) {
     if (bias) DLLM_HIP_TRY(hipMemcpyAsync(h->bias, bias, h->N * 4, hipMemcpyDeviceToDevice, st));
     dim3 gf(static_cast<unsigned>((h->Npad + 255) / 256), static_cast<unsigned>(h->K / 64));
     build_fragments_kernel<<<gf, 256, 0, st>>>(h->canon, h->K, h->N, h->Npad, h->bits, h->wdev);
+    DLLM_LAUNCH_CHECK();
+    dim3 gd(static_cast<unsigned>((h->Npad + 255) / 256), static_cast<unsigned>((h->K + 127) / 128));
+    build_decode_kernel<<<gd, 256, 0, st>>>(h->canon, h->K, h->N, h->Npad, h->bits, h->wdec);
     DLLM_LAUNCH_CHECK();
     dim3 gs(static_cast<unsigned>((h->Npad + 255) / 256), static_cast<unsigned>(h->G));
     build_sz_kernel<<<gs, 256, 0, st>>>(h->scales, h->zps, h->G, h->N, h->Npad, h->sz);
@@ -529,7 +758,14 @@ int dllm_linear_info(dllm_linear_t h, size_t *K, size_t *N, uint8_t *bits, size_
 
 size_t dllm_linear_weight_bytes(dllm_linear_t h) {
     if (!h) return 0;
-    return h->Npad * h->K * h->bits / 8 + h->G * h->Npad * 4;
+    return h->Npad * h->K * h->bits / 8 + h->G * h->Npad * 4;   // one layout is read per forward
+}
+
+int dllm_linear_set_kernel_variant(dllm_linear_t h, int variant) {
+    if (!h) return fail(DLLM_ERR_INVALID_PARAMS, "null handle");
+    if (variant < 0 || variant > 3) return fail(DLLM_ERR_INVALID_PARAMS, "variant must be 0..3");
+    h->variant = variant;
+    return DLLM_OK;
 }
 
 int dllm_linear_destroy(dllm_linear_t h) {

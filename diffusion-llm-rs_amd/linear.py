@@ -67,6 +67,10 @@ class QuantLinear:
         check(_lib.load().dllm_linear_export(self._h, _ptr(codes), _ptr(scales), _ptr(zps), _stream()))
         return codes, scales, zps
 
+    def set_kernel_variant(self, variant: int):
+        """Prefill GEMM schedule variant (tuning / A-B benchmarking)."""
+        check(_lib.load().dllm_linear_set_kernel_variant(self._h, int(variant)))
+
     def weight_bytes(self) -> int:
         return int(_lib.load().dllm_linear_weight_bytes(self._h))
 

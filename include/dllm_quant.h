@@ -161,6 +161,8 @@ int dllm_linear_export(dllm_linear_t h, uint8_t *packed_codes, float *scales, ui
 int dllm_linear_info(dllm_linear_t h, size_t *K, size_t *N, uint8_t *bits, size_t *group);
 /* HBM bytes the forward's GEMM kernel reads for the weights (packed codes + scales/zps). */
 size_t dllm_linear_weight_bytes(dllm_linear_t h);
+/* Tuning knob (benchmarks / A-B runs): selects the prefill GEMM schedule variant 0..3. */
+int dllm_linear_set_kernel_variant(dllm_linear_t h, int variant);
 int dllm_linear_destroy(dllm_linear_t h);
 
 /* ---- a9: int-quantized KV dequant-attention (consumer of QuantizedKVCacheEntry) -------------

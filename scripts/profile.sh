@@ -11,9 +11,12 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-f
 rc=$?; echo "kernel-trace rc=$rc"; tail -3 "$OUT/kt.log"
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1 || true
-for C in FETCH_SIZE WRITE_SIZE "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES" "SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS"; do
+SETS=${PMC_SETS:-"FETCH_SIZE;WRITE_SIZE;SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES;SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS"}
+IFS=';' read -ra SETARR <<< "$SETS"
+for C in "${SETARR[@]}"; do
   tag=$(echo $C | cut -d' ' -f1)
-  timeout -k 10 300 rocprofv3 --pmc $C --kernel-include-regex "${KREGEX:-wq_gemm}" -d "$OUT/pmc_$tag" -o pmc --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu > "$OUT/pmc_$tag.log" 2>&1
+  [ -n "$tag" ] || continue
+  timeout -k 10 300 rocprofv3 --pmc $C --kernel-include-regex "${KREGEX:-wq_gemm}" -d "$OUT/pmc_$tag" -o pmc --output-format csv -- python3 bench.py ${PMC_BENCH_ARGS:---steps 5 --warmup 2 --no-cpu} > "$OUT/pmc_$tag.log" 2>&1
   rc=$?; echo "pmc $tag rc=$rc"; tail -2 "$OUT/pmc_$tag.log"
   case $rc in 124|134|137|139) echo "hard failure; stopping"; exit $rc;; esac
 done
