@@ -16,15 +16,15 @@ from . import _lib
 from ._lib import (CalibrationRequired, HipError, InvalidParams, QuantizationError, ShapeMismatch,
                    UnsupportedOperation)
 from . import quantization, quant, kvquant, linear
-from .quantization import (QuantizedKVCacheEntry, QuantizedTensor, compression_ratio, dequantize_tensor, pack,
-                           quantize_tensor, unpack)
+from .quantization import (QuantizedKVCacheEntry, QuantizedTensor, compression_ratio, dequantize_tensor, kv_attention,
+                           pack, quantize_tensor, unpack)
 from .quant import CalibrationData, DefaultQuantizer, QuantizationParams, QuantizationType, quant_utils
 from .kvquant import BitQuantizer, PrefillKVQuant, SystemConfig, compress_vectors, decompress_vectors
 from .linear import MixedPrecisionStack, QuantLinear
 
 __all__ = [
     "quantize_tensor", "dequantize_tensor", "pack", "unpack", "compression_ratio", "QuantizedTensor",
-    "QuantizedKVCacheEntry", "QuantizationType", "QuantizationParams", "DefaultQuantizer", "quant_utils",
+    "QuantizedKVCacheEntry", "kv_attention", "QuantizationType", "QuantizationParams", "DefaultQuantizer", "quant_utils",
     "CalibrationData", "BitQuantizer", "PrefillKVQuant", "SystemConfig", "compress_vectors", "decompress_vectors",
     "QuantLinear", "MixedPrecisionStack", "QuantizationError", "InvalidParams", "UnsupportedOperation",
     "ShapeMismatch", "CalibrationRequired", "HipError",

@@ -487,6 +487,9 @@ __global__ void __launch_bounds__(kDecWaves * 64)
 wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdec,
                  const uint32_t *__restrict__ sz, const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad,
                  int group) {
+    // Slabs in flight per wave: every load of a round (W words, scales, X fragments) is issued
+    // before the first MFMA, so a round costs one memory latency, not one per 32-deep step.
+    constexpr int kDepth = MT <= 2 ? 4 : 2;
     __shared__ __attribute__((aligned(16))) float red[kDecWaves * MT * 64 * 4];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int n0 = blockIdx.x * 16;
@@ -495,25 +498,47 @@ wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
     const int ko = 8 * (lane >> 4);
     const uint32_t *wbase = wdec + (static_cast<size_t>(blockIdx.x) * nslab * 64 + lane) * BITS;
 
+    // Token rows beyond M contribute zeros: their lanes issue no X load at all (for M < 16 this
+    // removes most of the vector-memory traffic, which is what bounds this kernel).
     const __half *xrow[MT];
+    bool xvalid[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-        int m = mt * 16 + (lane & 15);
-        m = m < M ? m : M - 1;
-        xrow[mt] = X + static_cast<size_t>(m) * K + ko;
+        const int m = mt * 16 + (lane & 15);
+        xvalid[mt] = m < M;
+        xrow[mt] = X + static_cast<size_t>(m < M ? m : 0) * K + ko;
     }
+    // One scale word per (slab, 32-step) unless a group spans the whole slab (group % 128 == 0).
+    const bool slab_group = (group % 128) == 0;
 
     float4_t acc[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[mt] = float4_t{0.f, 0.f, 0.f, 0.f};
 
-    constexpr int kDepth = 4;   // slabs in flight per wave
     for (int base = wave; base < nslab; base += kDecWaves * kDepth) {
         uint32_t w[kDepth][BITS];
+        uint32_t szv[kDepth][4];
+        half8_t xb[kDepth][4][MT];
 #pragma unroll
         for (int i = 0; i < kDepth; ++i) {
             const int slab = base + i * kDecWaves;
-            if (slab < nslab) load_words<BITS>(w[i], wbase + static_cast<size_t>(slab) * 64 * BITS);
+            if (slab < nslab) {
+                load_words<BITS>(w[i], wbase + static_cast<size_t>(slab) * 64 * BITS);
+                if (slab_group) {
+                    const uint32_t v = sz[((slab * 128) / group) * Npad + ncol];
+                    szv[i][0] = szv[i][1] = szv[i][2] = szv[i][3] = v;
+                }
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const int k = min(slab * 128 + t * 32, K - 32);   // clamp: a step beyond K is skipped below
+                    if (!slab_group) szv[i][t] = sz[(k / group) * Npad + ncol];
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt) {
+                        xb[i][t][mt] = half8_t{0, 0, 0, 0, 0, 0, 0, 0};
+                        if (xvalid[mt]) xb[i][t][mt] = *reinterpret_cast<const half8_t *>(xrow[mt] + k);
+                    }
+                }
+            }
         }
 #pragma unroll
         for (int i = 0; i < kDepth; ++i) {
@@ -521,16 +546,13 @@ wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
             if (slab >= nslab) break;
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
-                const int k = slab * 128 + t * 32;
-                if (k >= K) break;
+                if (slab * 128 + t * 32 >= K) break;
                 half2_t nz, sc;
-                split_sz(sz[(k / group) * Npad + ncol], nz, sc);
+                split_sz(szv[i][t], nz, sc);
                 const half8_t a = dequant_frag<BITS>(w[i], t, nz, sc);
 #pragma unroll
-                for (int mt = 0; mt < MT; ++mt) {
-                    const half8_t b = *reinterpret_cast<const half8_t *>(xrow[mt] + k);
-                    acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, acc[mt], 0, 0, 0);
-                }
+                for (int mt = 0; mt < MT; ++mt)
+                    acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, xb[i][t][mt], acc[mt], 0, 0, 0);
             }
         }
     }

@@ -181,3 +181,22 @@ class QuantizedKVCacheEntry:
     def memory_usage(self) -> int:
         """Packed bytes of K and V (the accounting of diffuse-llm-rs/src/lib.rs:279-302)."""
         return sum(packed_bytes(t.numel(), t.bits) for t in (self.keys, self.values))
+
+
+def kv_attention(q: torch.Tensor, keys: QuantizedTensor, values: QuantizedTensor) -> torch.Tensor:
+    """Quantized-KV dequant-attention (a9): O = softmax(Q K^T / sqrt(D)) V per head with K, V the
+    per-tensor quantized cache tensors of ``QuantizedKVCacheEntry`` (packed, 4 or 8 bits),
+    dequantized inside the kernel.  q: f16 [S, H, 128] -> O f16 [S, H, 128]."""
+    if q.dim() != 3:
+        raise _lib.ShapeMismatch("q must be [S, H, D]")
+    S, H, D = q.shape
+    for t in (keys, values):
+        if not t.packed or t.numel() != S * H * D:
+            raise _lib.ShapeMismatch("keys/values must be packed [S, H, D] QuantizedTensors")
+    if keys.bits != values.bits:
+        raise _lib.InvalidParams("keys and values must share the bit width")
+    qd = _dev(q, torch.float16)
+    out = torch.empty(S, H, D, dtype=torch.float16, device=qd.device)
+    check(_lib.load().dllm_kv_attention(_ptr(qd), _ptr(keys.data), _ptr(keys.params), _ptr(values.data),
+                                        _ptr(values.params), keys.bits, S, H, D, _ptr(out), _stream()))
+    return out

@@ -1,0 +1,31 @@
+"""M-sweep of the quantized linear layer (K=N=4096 int4 g128).  Prints per-M event timings; run
+under `rocprofv3 --kernel-trace` and pass the trace to scripts/sweep_trace.py for pure kernel
+durations (no launch gaps).  Every M issues exactly WARM + REPS wq_* launches, in order."""
+import json, sys
+from pathlib import Path
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import torch
+import __graft_entry__ as g
+
+WARM, REPS = 5, 20
+Ms = [int(a) for a in sys.argv[1:]] or [1, 4, 16, 32, 64, 128, 256, 512, 1024, 2048, 4096, 8192]
+d = g.load_package()
+K = N = 4096
+torch.manual_seed(0)
+W = 0.02 * torch.randn(K, N, device="cuda")
+lin = d.QuantLinear.from_weight(W, None, 4, 128)
+torch.cuda.synchronize()
+for M in Ms:
+    X = torch.randn(M, K, device="cuda").half()
+    Y = torch.empty(M, N, dtype=torch.float16, device="cuda")
+    torch.cuda.synchronize()
+    for _ in range(WARM):
+        lin(X, out=Y)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(REPS):
+        lin(X, out=Y)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / REPS
+    print(json.dumps({"M": M, "event_us": round(ms * 1e3, 2)}), flush=True)

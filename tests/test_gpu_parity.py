@@ -292,3 +292,42 @@ def test_mixed_precision_stack(dllm, torch, orc):
         assert rel_err(host(y.float()), yr) <= REL_TOL, (i, rel_err(host(y.float()), yr))
         h = y
     assert torch.equal(stack(x), h)
+
+
+# ---- a9: quantized-KV dequant-attention ---------------------------------------------------------
+
+@pytest.mark.parametrize("S,H,bits", [(256, 2, 4), (200, 3, 4), (96, 1, 8), (512, 4, 4), (33, 2, 4)])
+def test_kv_attention_vs_oracle(dllm, torch, orc, S, H, bits):
+    """O = softmax(Q K^T/sqrt(128)) V with K, V per-tensor quantized (a1) and dequantized (a2) in
+    the kernel; oracle: f64 SDPA on the oracle-dequantized K, V and the same f16-rounded Q."""
+    rng = np.random.default_rng(S * 10 + H)
+    D = 128
+    Q = rng.standard_normal((S, H, D)).astype(np.float32).astype(np.float16)
+    K = rng.standard_normal((S, H, D)).astype(np.float32)
+    V = (rng.standard_normal((S, H, D)) * 2 + 0.5).astype(np.float32)
+    kq = dllm.QuantizedTensor.quantize(dev(torch, K), bits, packed=True)
+    vq = dllm.QuantizedTensor.quantize(dev(torch, V), bits, packed=True)
+    O = host(dllm.kv_attention(dev(torch, Q), kq, vq).float())
+    Kh = orc.dequantize_tensor(*orc.quantize_tensor(K, bits)).reshape(S, H, D)
+    Vh = orc.dequantize_tensor(*orc.quantize_tensor(V, bits)).reshape(S, H, D)
+    Oref = orc.attention(Q.astype(np.float32), Kh, Vh)
+    assert rel_err(O, Oref) <= REL_TOL, rel_err(O, Oref)
+
+
+def test_kv_attention_peaked_softmax(dllm, torch, orc):
+    """A key that dominates one query forces the online-softmax rescale branch at a chosen block
+    (rule: a rare data-dependent branch needs its own test)."""
+    S, H, D = 256, 1, 128
+    rng = np.random.default_rng(3)
+    Q = (rng.standard_normal((S, H, D)) * 0.1).astype(np.float16)
+    K = (rng.standard_normal((S, H, D)) * 0.1).astype(np.float32)
+    V = rng.standard_normal((S, H, D)).astype(np.float32)
+    K[200, 0, :] = 8.0 * np.sign(Q[5, 0, :].astype(np.float32))   # key 200 (7th block) spikes query 5
+    kq = dllm.QuantizedTensor.quantize(dev(torch, K), 8, packed=True)
+    vq = dllm.QuantizedTensor.quantize(dev(torch, V), 8, packed=True)
+    O = host(dllm.kv_attention(dev(torch, Q), kq, vq).float())
+    Kh = orc.dequantize_tensor(*orc.quantize_tensor(K, 8)).reshape(S, H, D)
+    Vh = orc.dequantize_tensor(*orc.quantize_tensor(V, 8)).reshape(S, H, D)
+    Oref = orc.attention(Q.astype(np.float32), Kh, Vh)
+    assert rel_err(O, Oref) <= REL_TOL
+    assert rel_err(O[5], Oref[5]) <= REL_TOL
