@@ -15,7 +15,7 @@ this package is the host-side mirror of the reference's Rust operator surface:
 from . import _lib
 from ._lib import (CalibrationRequired, HipError, InvalidParams, QuantizationError, ShapeMismatch,
                    UnsupportedOperation)
-from . import quantization, quant, kvquant, linear
+from . import quantization, quant, kvquant, linear, parallel
 from .quantization import (QuantizedKVCacheEntry, QuantizedTensor, compression_ratio, dequantize_tensor, kv_attention,
                            pack, quantize_tensor, unpack)
 from .quant import CalibrationData, DefaultQuantizer, QuantizationParams, QuantizationType, quant_utils

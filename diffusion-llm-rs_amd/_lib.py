@@ -96,6 +96,15 @@ SIGNATURES = {
     "dllm_linear_set_kernel_variant": (INT, [P, INT]),
     "dllm_linear_destroy": (INT, [P]),
     "dllm_kv_attention": (INT, [P, P, P, P, P, U8, S, S, S, P, P]),
+    "dllm_quantize_tensor_host": (INT, [P, S, U8, P, P, P]),
+    "dllm_dequantize_tensor_host": (INT, [P, S, FL, FL, P]),
+    "dllm_default_quantize_host": (INT, [P, S, INT, FL, I32, P]),
+    "dllm_default_dequantize_host": (INT, [P, S, FL, I32, P]),
+    "dllm_bit_quantize_host": (INT, [P, S, U32, FL, FL, P]),
+    "dllm_bit_dequantize_host": (INT, [P, S, FL, FL, P]),
+    "dllm_compress_vector_host": (INT, [P, S, U8, P, P, P]),
+    "dllm_linear_create_host": (INT, [P, P, S, S, U8, S, P]),
+    "dllm_linear_forward_host": (INT, [P, P, S, P]),
 }
 
 _lib = None

@@ -176,6 +176,25 @@ int dllm_kv_attention(const void *Q, const uint8_t *Kq, const float *k_params, c
                       const float *v_params, uint8_t bits, size_t S, size_t H, size_t D, void *O,
                       dllm_stream_t stream);
 
+/* ---- host-slice variants (synchronous; stage through device memory; not graph-capturable) ----
+ * The literal shapes of the reference's Rust signatures, for callers holding host slices. */
+/* quantize_tensor(&[f32], u8) -> (Vec<u8>, f32, f32): codes one per byte (quantization.rs:38-68). */
+int dllm_quantize_tensor_host(const float *x, size_t n, uint8_t bits, uint8_t *codes, float *scale, float *zp);
+/* dequantize_tensor(&[u8], f32, f32) -> Vec<f32> (quantization.rs:81-85). */
+int dllm_dequantize_tensor_host(const uint8_t *codes, size_t n, float scale, float zp, float *out);
+/* DefaultQuantizer quantize / dequantize (quantization/src/quantize.rs:111-184). */
+int dllm_default_quantize_host(const float *x, size_t n, int qtype, float scale, int32_t zero_point, uint8_t *out);
+int dllm_default_dequantize_host(const uint8_t *q, size_t n, float scale, int32_t zero_point, float *out);
+/* kvquant::BitQuantizer::{quantize, dequantize} (prefill-kvquant-rs/lib.rs:39-53). */
+int dllm_bit_quantize_host(const float *x, size_t n, uint32_t bits, float scale, float zero_point, uint8_t *out);
+int dllm_bit_dequantize_host(const uint8_t *q, size_t n, float scale, float zero_point, float *out);
+/* diffusion_prefill KVCache::compress_vector (diffusion_prefill/src/prefill_kv.rs:104-121). */
+int dllm_compress_vector_host(const float *x, size_t n, uint8_t bits, uint8_t *out, float *scale, float *zp);
+/* SimpleDiffusionModel::new + forward (diffuse-llm-rs/src/lib.rs:791-813) with quantized W. */
+int dllm_linear_create_host(const float *W, const float *bias, size_t K, size_t N, uint8_t bits, size_t group,
+                            dllm_linear_t *out);
+int dllm_linear_forward_host(dllm_linear_t h, const float *X, size_t M, float *Y);
+
 #ifdef __cplusplus
 }
 #endif

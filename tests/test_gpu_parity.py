@@ -331,3 +331,24 @@ def test_kv_attention_peaked_softmax(dllm, torch, orc):
     Oref = orc.attention(Q.astype(np.float32), Kh, Vh)
     assert rel_err(O, Oref) <= REL_TOL
     assert rel_err(O[5], Oref[5]) <= REL_TOL
+
+
+# ---- host-slice entry points (the literal Rust signatures) ---------------------------------------
+
+def test_host_entry_points(dllm, orc):
+    import ctypes as C
+    L = dllm._lib.load()
+    rng = np.random.default_rng(21)
+    x = (rng.standard_normal(1001) * 2).astype(np.float32)
+    q = np.zeros(x.size, np.uint8)
+    s, z = C.c_float(), C.c_float()
+    assert L.dllm_quantize_tensor_host(x.ctypes.data, x.size, 4, q.ctypes.data, C.byref(s), C.byref(z)) == 0
+    rq, rs, rz = orc.quantize_tensor(x, 4)
+    assert np.array_equal(q, rq) and np.float32(s.value) == rs and np.float32(z.value) == rz
+    y = np.zeros(x.size, np.float32)
+    assert L.dllm_dequantize_tensor_host(q.ctypes.data, q.size, s.value, z.value, y.ctypes.data) == 0
+    assert same_bits(y, orc.dequantize_tensor(rq, rs, rz))
+    assert L.dllm_bit_quantize_host(x.ctypes.data, x.size, 4, 0.25, -1.0, q.ctypes.data) == 0
+    assert np.array_equal(q, orc.bit_quantize(x, 4, 0.25, -1.0))
+    assert L.dllm_default_quantize_host(x.ctypes.data, x.size, 0, 0.5, 3, q.ctypes.data) == 0
+    assert np.array_equal(q, orc.default_quantize(x, 0, 0.5, 3))
