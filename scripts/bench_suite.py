@@ -1,0 +1,145 @@
+"""Measurement suite for every BASELINE.json config on one MI355X (JSON lines on stdout).
+
+C1  int8 DefaultQuantizer quantize -> dequantize round trip, 1024x1024 (HBM-bound kernels)
+C2  int4 g128 dequant+GEMM, M = 2048 / 4096, K = N = 4096 (MFMA-bound) + M-sweep
+C2' standalone per-tensor quantize (min/max + quantize+pack) and dequant of an 8192x4096 f32 tensor
+C3  int2/int4 mixed 12-layer stack, seq 4096, d 4096
+C4  int4 KV quantize (K and V, per tensor) + dequant-attention, S 8192, 32 heads x 128
+Timings: HIP events on the launch stream over back-to-back launches (includes launch gaps);
+run under `rocprofv3 --kernel-trace --stats` for per-kernel durations.
+"""
+import json
+import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import numpy as np
+import torch
+
+import __graft_entry__ as g
+
+d = g.load_package()
+dev = torch.device("cuda")
+HBM = 8.0e12
+PEAK = 2.5e15
+
+
+def timed(fn, reps=20, warm=5):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e-3   # seconds
+
+
+def emit(**kw):
+    print(json.dumps(kw), flush=True)
+
+
+def prewarm(seconds=0.3):
+    a = torch.randn(4096, 4096, device=dev, dtype=torch.float16)
+    t0 = time.time()
+    while time.time() - t0 < seconds:
+        a = a @ a
+        a = a / a.norm()
+    torch.cuda.synchronize()
+
+
+def c1():
+    x = torch.randn(1024 * 1024, device=dev)
+    q = d.DefaultQuantizer(8, True, None)
+    t = q.quantize(x, d.QuantizationType.Int8)
+    sq = timed(lambda: q.quantize(x, d.QuantizationType.Int8))
+    sd = timed(lambda: t.dequantize())
+    n = x.numel()
+    emit(config="C1 int8 DefaultQuantizer 1024x1024", quantize_us=round(sq * 1e6, 2),
+         quantize_GBs=round(5 * n / sq / 1e9, 1), dequantize_us=round(sd * 1e6, 2),
+         dequantize_GBs=round(5 * n / sd / 1e9, 1), note="includes torch allocation + launch per call")
+
+
+def c2():
+    K = N = 4096
+    W = 0.02 * torch.randn(K, N, device=dev)
+    lin = d.QuantLinear.from_weight(W, None, 4, 128)
+    for M in (2048, 4096):
+        X = torch.randn(M, K, device=dev).half()
+        Y = torch.empty(M, N, dtype=torch.float16, device=dev)
+        s = timed(lambda: lin(X, out=Y))
+        b = K * N // 2 + (K // 128) * N * 5 + M * K * 2 + M * N * 2
+        emit(config=f"C2 int4 g128 dequant+GEMM M={M} K=N=4096", us=round(s * 1e6, 1),
+             tflops=round(2 * M * N * K / s / 1e12, 1), mfma_frac=round(2 * M * N * K / s / PEAK, 3),
+             tok_per_s=round(M / s), GiBs=round(b / s / 2**30, 1))
+    for M in (1, 16, 64, 256):
+        X = torch.randn(M, K, device=dev).half()
+        Y = torch.empty(M, N, dtype=torch.float16, device=dev)
+        s = timed(lambda: lin(X, out=Y))
+        b = K * N // 2 + (K // 128) * N * 5 + M * K * 2 + M * N * 2
+        emit(config=f"C2 sweep M={M}", us=round(s * 1e6, 2), GBs=round(b / s / 1e9, 1),
+             hbm_frac=round(b / s / HBM, 3), tflops=round(2 * M * N * K / s / 1e12, 1))
+
+
+def c2p():
+    n = 8192 * 4096
+    x = torch.randn(n, device=dev)
+    L = d._lib.load()
+    out = torch.empty(n // 2, dtype=torch.uint8, device=dev)
+    params = torch.empty(2, dtype=torch.float32, device=dev)
+    ws = torch.empty(L.dllm_quantize_tensor_workspace(n), dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+
+    def q():
+        L.dllm_quantize_tensor(x.data_ptr(), n, 4, 1, out.data_ptr(), params.data_ptr(), ws.data_ptr(), ws.numel(), st)
+    s = timed(q)
+    emit(config="C2' quantize_tensor f32 8192x4096 -> int4 packed (min/max + quantize)", us=round(s * 1e6, 1),
+         GBs_algorithmic=round((4 * n + n / 2) / s / 1e9, 1), hbm_frac=round((4 * n + n / 2) / s / HBM, 3),
+         note="algorithmic bytes count the f32 read once; the min/max pass reads it a second time")
+    y = torch.empty(n, dtype=torch.float16, device=dev)
+
+    def dq():
+        L.dllm_dequantize_tensor(out.data_ptr(), n, 4, 1, params.data_ptr(), y.data_ptr(), 1, st)
+    s = timed(dq)
+    emit(config="C2' dequantize int4 packed -> f16, 8192x4096", us=round(s * 1e6, 1),
+         GBs=round((n / 2 + 2 * n) / s / 1e9, 1), hbm_frac=round((n / 2 + 2 * n) / s / HBM, 3))
+
+
+def c3():
+    dm, M, Lyr = 4096, 4096, 12
+    Ws = [0.02 * torch.randn(dm, dm, device=dev) for _ in range(Lyr)]
+    stack = d.MixedPrecisionStack(Ws, bits=(2, 4))
+    del Ws
+    X = torch.randn(M, dm, device=dev).half()
+    s = timed(lambda: stack(X), reps=5, warm=2)
+    emit(config="C3 int2/int4 mixed 12-layer stack seq 4096 d 4096", ms=round(s * 1e3, 3),
+         tflops=round(Lyr * 2 * M * dm * dm / s / 1e12, 1), tok_per_s=round(M / s))
+
+
+def c4():
+    S, H, D = 8192, 32, 128
+    K = torch.randn(S, H, D, device=dev)
+    V = torch.randn(S, H, D, device=dev)
+    Q = torch.randn(S, H, D, device=dev).half()
+
+    def kvq():
+        return d.QuantizedKVCacheEntry.new(K, V, 4)
+    s = timed(kvq, reps=10, warm=3)
+    n = S * H * D
+    emit(config="C4 KV quantize (K and V per tensor, int4 packed) S8192 H32 D128", us=round(s * 1e6, 1),
+         GBs_algorithmic=round(2 * (4 * n + n / 2) / s / 1e9, 1))
+    e = kvq()
+    s = timed(lambda: d.kv_attention(Q, e.keys, e.values), reps=5, warm=2)
+    fl = 4 * S * S * H * D
+    emit(config="C4 int4 dequant-attention S8192 H32 D128", ms=round(s * 1e3, 3),
+         tflops=round(fl / s / 1e12, 1), mfma_frac=round(fl / s / PEAK, 3))
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["c1", "c2", "c2p", "c3", "c4"]
+    prewarm()
+    for w in which:
+        globals()[w]()
