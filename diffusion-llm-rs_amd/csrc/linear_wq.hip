@@ -42,7 +42,7 @@ struct dllm_linear {
     float *bias = nullptr;        // [Npad]
     __half *xws = nullptr;        // f32 -> f16 staging for X
     size_t xws_elems = 0;
-    int variant = 3;              // prefill schedule variant (tuning knob, see wq_gemm_kernel)
+    int variant = 4;              // prefill schedule variant (tuning knob, see wq_gemm_kernel)
     std::mutex mu;
 };
 
@@ -472,6 +472,197 @@ wq_gemm_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__res
 }
 
 // ---------------------------------------------------------------------------------------------
+// Big-tile prefill GEMM (used when it still fills the chip): block tile 256 (m) x 256 (n), 8 waves
+// side by side in n (wave tile 256 x 32 as above), so each X tile is shared by 8 waves (half the
+// LDS-DMA per FLOP of the 128-column tile).  Three LDS stages in a ring: stage kt+2 is issued
+// while kt is computed, the end-of-step wait is a COUNTED vmcnt that leaves kt+2's DMAs in flight
+// across the raw s_barrier (never __syncthreads, whose fence would drain them).
+// ---------------------------------------------------------------------------------------------
+// LDS-DMA issued from inline asm: invisible to hipcc's waitcnt pass, so the only waits on these
+// loads are the counted vmcnt statements placed by hand (guide 5.7, M0 written in the statement).
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+    return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_ptr)(const_cast<void *>(p))));
+}
+__device__ __forceinline__ void glds16_asm(const void *gsrc, uint32_t lds_dst) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+__device__ __forceinline__ void glds4_asm(const void *gsrc, uint32_t lds_dst) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+
+constexpr int kBN8 = 256;
+
+template <int BITS>
+struct StageLayout8 {
+    static constexpr int kX = kBM * kBK * 2;            // 32 KiB
+    static constexpr int kW = 8 * 64 * BITS * 4;        // 8 waves
+    static constexpr int kSZ = 8 * 64 * 4;
+    static constexpr int kBytes = kX + kW + kSZ;
+    // LDS-DMA instructions per wave per stage: 4 X rounds + weight words + 1 scale dword.
+    static constexpr int kOps = 4 + (BITS == 4 ? 1 : 2) + 1;
+};
+
+template <int BITS, typename YT>
+__global__ void __launch_bounds__(512, 1)
+wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdev,
+                const uint32_t *__restrict__ sz, const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad,
+                int group, int nbm, int nbn) {
+    using SL = StageLayout8<BITS>;
+    __shared__ __attribute__((aligned(16))) uint8_t st0[SL::kBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t st1[SL::kBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t st2[SL::kBytes];
+
+    const int nb = nbm * nbn, orig = blockIdx.x;
+    const int xcd = orig % kXCDs, q8 = nb / kXCDs, r8 = nb % kXCDs;
+    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / kXCDs;
+    const int bm = wgid / nbn, bn = wgid % nbn;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int m0 = bm * kBM, n0 = bn * kBN8;
+    const unsigned nk = static_cast<unsigned>(K) / kBK;
+    const unsigned kpg = static_cast<unsigned>(group) / kBK;
+    const unsigned nt = static_cast<unsigned>(n0 + wave * 32) >> 5;
+    const int ncol = n0 + wave * 32 + (lane & 31);
+
+    // X: 4 rounds x 8 KiB (512 threads x 16 B); round i, wave w covers rows 64 i + 8 w .. +8.
+    const int chunk_st = lane & 7;
+    const __half *xsrc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int row = i * 64 + wave * 8 + (lane >> 3);
+        int grow = m0 + row;
+        grow = grow < M ? grow : M - 1;
+        const int c = chunk_st ^ ((row >> 1) & 7);
+        xsrc[i] = X + static_cast<size_t>(grow) * K + c * 8;
+    }
+    const uint32_t *wsrc = wdev + (static_cast<size_t>(nt) * nk * 64 + lane) * BITS;
+    const uint32_t *szsrc = sz + ncol;
+
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(wave);
+    auto stage = [&](uint8_t *sb, unsigned kt) {
+        const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(sb));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) glds16_asm(xsrc[i] + kt * kBK, base + wv * 1024 + i * 8192);
+        const uint32_t *wp = wsrc + static_cast<size_t>(kt) * 64 * BITS;
+        const uint32_t wb = base + SL::kX + wv * (64 * BITS * 4);
+        if constexpr (BITS == 4) {
+            glds16_asm(wp, wb);
+        } else if constexpr (BITS == 8) {
+            glds16_asm(wp, wb);
+            glds16_asm(wp + 4, wb + 64 * 16);
+        } else {
+            glds4_asm(wp, wb);
+            glds4_asm(wp + 1, wb + 256);
+        }
+        glds4_asm(szsrc + (kt / kpg) * Npad, base + SL::kX + SL::kW + wv * 256);
+    };
+
+    float16_t acc[kMReps];
+#pragma unroll
+    for (int r = 0; r < kMReps; ++r)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[r][e] = 0.0f;
+
+    const int hsel = lane >> 5;
+    const int rowx = ((lane & 31) >> 1) & 7;
+    int soff[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) soff[s] = (lane & 31) * (kBK * 2) + ((((2 * s + hsel) ^ rowx)) << 4);
+
+    auto read_b = [&](half8_t (&b)[kMReps], const uint8_t *sb, int s) {
+#pragma unroll
+        for (int r = 0; r < kMReps; ++r) b[r] = *reinterpret_cast<const half8_t *>(sb + soff[s] + r * 32 * kBK * 2);
+    };
+    auto mfma8 = [&](const half8_t &a, const half8_t (&b)[kMReps]) {
+#pragma unroll
+        for (int r = 0; r < kMReps; ++r) acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b[r], acc[r], 0, 0, 0);
+    };
+    // Compute stage `sb`; stage `pf` receives k-step kt+2.
+    auto step = [&](const uint8_t *sb, uint8_t *pf, unsigned kt) {
+        const bool issue = kt + 2 < nk;
+        if (issue) stage(pf, kt + 2);
+        uint32_t w[BITS];
+        lds_words<BITS>(w, sb + SL::kX + wave * (64 * BITS * 4), lane);
+        half2_t nz, sc;
+        split_sz(*reinterpret_cast<const uint32_t *>(sb + SL::kX + SL::kW + wave * 256 + lane * 4), nz, sc);
+        half8_t bA[kMReps], bB[kMReps];
+        read_b(bA, sb, 0);
+        half8_t aA = dequant_frag<BITS>(w, 0, nz, sc), aB;
+        auto sub = [&](half8_t (&bc)[kMReps], half8_t (&bn)[kMReps], const half8_t &ac, half8_t &an, int s) {
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_setprio(1);
+            if (s < 3) {
+                read_b(bn, sb, s + 1);
+                an = dequant_frag<BITS>(w, s + 1, nz, sc);
+            }
+            mfma8(ac, bc);
+#pragma unroll
+            for (int i = 0; i < kMReps; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+            }
+            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        sub(bA, bB, aA, aB, 0);
+        sub(bB, bA, aB, aA, 1);
+        sub(bA, bB, aA, aB, 2);
+        sub(bB, bA, aB, aA, 3);
+        // Stage kt+1 must have landed; kt+2's DMAs may stay in flight across the barrier.
+        if (issue) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kOps) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    stage(st0, 0);
+    if (nk > 1) stage(st1, 1);
+    if (nk > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kOps) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    for (unsigned kt = 0; kt < nk; kt += 3) {
+        step(st0, st2, kt);
+        if (kt + 1 < nk) step(st1, st0, kt + 1);
+        if (kt + 2 < nk) step(st2, st1, kt + 2);
+    }
+
+    const int nb0 = n0 + wave * 32 + 4 * hsel;
+    float4 bv[4];
+#pragma unroll
+    for (int qd = 0; qd < 4; ++qd) bv[qd] = *reinterpret_cast<const float4 *>(bias + nb0 + 8 * qd);
+    const bool full = (m0 + kBM <= M) && (n0 + kBN8 <= N) && (N % 4) == 0;
+    if (full) {
+#pragma unroll
+        for (int r = 0; r < kMReps; ++r) {
+            YT *yrow = Y + static_cast<size_t>(m0 + r * 32 + (lane & 31)) * N + nb0;
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd)
+                store4<YT>(yrow + 8 * qd, acc[r][4 * qd + 0] + bv[qd].x, acc[r][4 * qd + 1] + bv[qd].y,
+                           acc[r][4 * qd + 2] + bv[qd].z, acc[r][4 * qd + 3] + bv[qd].w);
+        }
+    } else {
+        const bool vec_ok = (N % 4) == 0;
+#pragma unroll
+        for (int r = 0; r < kMReps; ++r) {
+            const int m = m0 + r * 32 + (lane & 31);
+            if (m >= M) continue;
+            YT *yrow = Y + static_cast<size_t>(m) * N;
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd)
+                store_out4<YT>(yrow, bias, nb0 + 8 * qd, N, vec_ok, acc[r][4 * qd + 0], acc[r][4 * qd + 1],
+                               acc[r][4 * qd + 2], acc[r][4 * qd + 3]);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Decode GEMM (small M, weight-streaming / HBM-bound): one block per 16-column n-tile
 // (N/16 blocks = 256 at N = 4096, one per CU), 8 waves split K by 128-deep slabs, 16x16x32
 // f16 MFMA with the weight as A (16 columns) and MT 16-token tiles of X as B, then the 8 wave
@@ -600,6 +791,14 @@ void launch_prefill(const dllm_linear *h, const __half *X, int M, YT *Y, hipStre
 template <int BITS, typename YT>
 int launch_gemm_t(const dllm_linear *h, const __half *X, size_t M, YT *Y, hipStream_t st) {
     if (M <= static_cast<size_t>(kDecodeMaxM)) return launch_decode<BITS, YT>(h, X, M, Y, st);
+    const int nbm8 = static_cast<int>((M + kBM - 1) / kBM), nbn8 = static_cast<int>((h->Npad + kBN8 - 1) / kBN8);
+    const bool big_ok = (h->Npad % kBN8) == 0 && nbm8 * nbn8 >= kCUs;
+    if ((h->variant == 4 || h->variant == 5) && big_ok) {
+        wq_gemm8_kernel<BITS, YT><<<static_cast<unsigned>(nbm8 * nbn8), 512, 0, st>>>(
+            X, (int)M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm8, nbn8);
+        DLLM_LAUNCH_CHECK();
+        return DLLM_OK;
+    }
     switch (h->variant) {
     case 0: launch_prefill<BITS, YT, 0>(h, X, (int)M, Y, st); break;
     case 1: launch_prefill<BITS, YT, 1>(h, X, (int)M, Y, st); break;
@@ -785,7 +984,7 @@ size_t dllm_linear_weight_bytes(dllm_linear_t h) {
 
 int dllm_linear_set_kernel_variant(dllm_linear_t h, int variant) {
     if (!h) return fail(DLLM_ERR_INVALID_PARAMS, "null handle");
-    if (variant < 0 || variant > 3) return fail(DLLM_ERR_INVALID_PARAMS, "variant must be 0..3");
+    if (variant < 0 || variant > 5) return fail(DLLM_ERR_INVALID_PARAMS, "variant must be 0..5");
     h->variant = variant;
     return DLLM_OK;
 }

@@ -352,3 +352,18 @@ def test_host_entry_points(dllm, orc):
     assert np.array_equal(q, orc.bit_quantize(x, 4, 0.25, -1.0))
     assert L.dllm_default_quantize_host(x.ctypes.data, x.size, 0, 0.5, 3, q.ctypes.data) == 0
     assert np.array_equal(q, orc.default_quantize(x, 0, 0.5, 3))
+
+
+def test_gemm_variants_bit_identical(dllm, torch):
+    """All prefill schedules (0..3: 256x128 tile; 4: 256x256 tile, 3-stage LDS ring) accumulate in
+    the same k order, so they must agree bit for bit -- including a ragged M tail."""
+    K, N, M = 1024, 4096, 4352
+    g = torch.Generator(device="cuda").manual_seed(8)
+    W = 0.02 * torch.randn(K, N, device="cuda", generator=g)
+    X = torch.randn(M, K, device="cuda", generator=g).half()
+    lin = dllm.QuantLinear.from_weight(W, 0.1 * torch.randn(N, device="cuda", generator=g), 4, 128)
+    outs = {}
+    for v in (0, 3, 4):
+        lin.set_kernel_variant(v)
+        outs[v] = lin(X, out_dtype=torch.float32)
+    assert torch.equal(outs[0], outs[3]) and torch.equal(outs[0], outs[4])
