@@ -43,6 +43,7 @@ struct dllm_linear {
     __half *xws = nullptr;        // f32 -> f16 staging for X
     size_t xws_elems = 0;
     int variant = 4;              // prefill schedule variant (tuning knob, see wq_gemm_kernel)
+    int dlab = 0;                 // decode-kernel ablation mask (measurement only; 0 in production)
     std::mutex mu;
 };
 
@@ -673,34 +674,41 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
 typedef float float4_t __attribute__((ext_vector_type(4)));
 constexpr int kDecWaves = 8;
 
-template <int BITS, typename YT, int MT>
+template <int BITS, typename YT, int MT, int LAB = 0>
 __global__ void __launch_bounds__(kDecWaves * 64)
 wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdec,
                  const uint32_t *__restrict__ sz, const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad,
                  int group) {
     // Slabs in flight per wave: every load of a round (W words, scales, X fragments) is issued
     // before the first MFMA, so a round costs one memory latency, not one per 32-deep step.
+    // The load phase has no branch and every loop bound is wave-uniform (scalar wave index): a
+    // per-lane branch around a load makes the compiler wait for it at the join, which serialises
+    // the rounds into one HBM latency per slab.  Rows >= M, steps past K and the clamped duplicate
+    // slabs of the last round read X through a buffer resource with an out-of-range offset, which
+    // returns zeros without a memory access; X is thereby also free of per-lane selects.
     constexpr int kDepth = MT <= 2 ? 4 : 2;
+    constexpr uint32_t kOOB = 0x80000000u;
     __shared__ __attribute__((aligned(16))) float red[kDecWaves * MT * 64 * 4];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int n0 = blockIdx.x * 16;
     const int nslab = (K + 127) / 128;
-    const int ncol = n0 + (lane & 15);
-    const int ko = 8 * (lane >> 4);
     const uint32_t *wbase = wdec + (static_cast<size_t>(blockIdx.x) * nslab * 64 + lane) * BITS;
-
-    // Token rows beyond M contribute zeros: their lanes issue no X load at all (for M < 16 this
-    // removes most of the vector-memory traffic, which is what bounds this kernel).
-    const __half *xrow[MT];
-    bool xvalid[MT];
+    // Scales: one dword per lane per slab, lane l fetching (column l & 15, 32-deep step l >> 4);
+    // step t's value for column c is then pulled from lane c + 16 t.
+    const uint32_t *szcol = sz + n0 + (lane & 15);
+    const int sz_step = lane >> 4;
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<__half *>(X), 0, static_cast<int>(static_cast<size_t>(M) * K * 2), 0x00020000);
+    uint32_t xoff[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
         const int m = mt * 16 + (lane & 15);
-        xvalid[mt] = m < M;
-        xrow[mt] = X + static_cast<size_t>(m < M ? m : 0) * K + ko;
+        xoff[mt] = m < M ? static_cast<uint32_t>((m * K + 8 * (lane >> 4)) * 2) : kOOB;
     }
-    // One scale word per (slab, 32-step) unless a group spans the whole slab (group % 128 == 0).
-    const bool slab_group = (group % 128) == 0;
+    // The epilogue's bias is fetched now, behind the weight stream, not after the reduction.
+    const int nb0 = n0 + 4 * (lane >> 4);
+    const float4 bv = *reinterpret_cast<const float4 *>(bias + nb0);
 
     float4_t acc[MT];
 #pragma unroll
@@ -708,38 +716,48 @@ wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
 
     for (int base = wave; base < nslab; base += kDecWaves * kDepth) {
         uint32_t w[kDepth][BITS];
-        uint32_t szv[kDepth][4];
+        uint32_t szl[kDepth];
         half8_t xb[kDepth][4][MT];
 #pragma unroll
         for (int i = 0; i < kDepth; ++i) {
-            const int slab = base + i * kDecWaves;
-            if (slab < nslab) {
+            const int slab_raw = base + i * kDecWaves;
+            const int slab = min(slab_raw, nslab - 1);
+            if constexpr (LAB & 4) {
+#pragma unroll
+                for (int j = 0; j < BITS; ++j) w[i][j] = lane * 0x01010101u + j + slab;
+            } else {
                 load_words<BITS>(w[i], wbase + static_cast<size_t>(slab) * 64 * BITS);
-                if (slab_group) {
-                    const uint32_t v = sz[((slab * 128) / group) * Npad + ncol];
-                    szv[i][0] = szv[i][1] = szv[i][2] = szv[i][3] = v;
-                }
+            }
+            const int ks = min(slab * 128 + sz_step * 32, K - 32);
+            if constexpr (LAB & 2) szl[i] = 0x3c00e400u + ks;
+            else szl[i] = szcol[static_cast<size_t>(ks / group) * Npad];
 #pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const int k = min(slab * 128 + t * 32, K - 32);   // clamp: a step beyond K is skipped below
-                    if (!slab_group) szv[i][t] = sz[(k / group) * Npad + ncol];
+            for (int t = 0; t < 4; ++t) {
+                const int k = slab_raw * 128 + t * 32;
+                const bool step_ok = slab_raw < nslab && k < K;
 #pragma unroll
-                    for (int mt = 0; mt < MT; ++mt) {
-                        xb[i][t][mt] = half8_t{0, 0, 0, 0, 0, 0, 0, 0};
-                        if (xvalid[mt]) xb[i][t][mt] = *reinterpret_cast<const half8_t *>(xrow[mt] + k);
+                for (int mt = 0; mt < MT; ++mt) {
+                    if constexpr (LAB & 1) {
+                        xb[i][t][mt] = half8_t{(_Float16)k, 1, 1, 1, 1, 1, 1, (_Float16)lane};
+                    } else {
+                        const uint32_t off = step_ok ? xoff[mt] + static_cast<uint32_t>(k * 2) : kOOB;
+                        xb[i][t][mt] = __builtin_bit_cast(
+                            half8_t, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
                     }
                 }
             }
         }
+        // Keep the scheduler from sinking the loads back next to their MFMAs (it does so to cut
+        // register pressure, which turns the round into one serial latency per fragment).
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < kDepth; ++i) {
-            const int slab = base + i * kDecWaves;
-            if (slab >= nslab) break;
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
-                if (slab * 128 + t * 32 >= K) break;
+                const uint32_t szv = static_cast<uint32_t>(
+                    __builtin_amdgcn_ds_bpermute(((lane & 15) + 16 * t) * 4, static_cast<int>(szl[i])));
                 half2_t nz, sc;
-                split_sz(szv[i][t], nz, sc);
+                split_sz(szv, nz, sc);
                 const half8_t a = dequant_frag<BITS>(w[i], t, nz, sc);
 #pragma unroll
                 for (int mt = 0; mt < MT; ++mt)
@@ -757,9 +775,18 @@ wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
 #pragma unroll
         for (int w = 0; w < kDecWaves; ++w) s += *reinterpret_cast<const float4_t *>(red + ((w * MT + mt) * 64 + lane) * 4);
         const int m = mt * 16 + (lane & 15);
-        if (m < M)
-            store_out4<YT>(Y + static_cast<size_t>(m) * N, bias, n0 + 4 * (lane >> 4), N, (N % 4) == 0, s[0], s[1],
-                           s[2], s[3]);
+        if (m < M && nb0 < N) {
+            YT *yrow = Y + static_cast<size_t>(m) * N;
+            const float y0 = s[0] + bv.x, y1 = s[1] + bv.y, y2 = s[2] + bv.z, y3 = s[3] + bv.w;
+            if ((N % 4) == 0) {
+                store4<YT>(yrow + nb0, y0, y1, y2, y3);
+            } else {
+                store1<YT>(yrow + nb0, y0);
+                if (nb0 + 1 < N) store1<YT>(yrow + nb0 + 1, y1);
+                if (nb0 + 2 < N) store1<YT>(yrow + nb0 + 2, y2);
+                if (nb0 + 3 < N) store1<YT>(yrow + nb0 + 3, y3);
+            }
+        }
     }
 }
 
@@ -770,7 +797,14 @@ int launch_decode(const dllm_linear *h, const __half *X, size_t M, YT *Y, hipStr
     const unsigned nb = static_cast<unsigned>(h->Npad / 16);
     const int Mi = static_cast<int>(M), K = static_cast<int>(h->K), N = static_cast<int>(h->N);
     const int Np = static_cast<int>(h->Npad), gr = static_cast<int>(h->group);
-    if (M <= 16)
+    if (M <= 16 && h->dlab != 0) {
+        switch (h->dlab) {
+#define DLLM_DLAB(L) case L: wq_decode_kernel<BITS, YT, 1, L><<<nb, kDecWaves * 64, 0, st>>>(X, Mi, K, h->wdec, h->sz, h->bias, Y, N, Np, gr); break;
+            DLLM_DLAB(1) DLLM_DLAB(2) DLLM_DLAB(3) DLLM_DLAB(4) DLLM_DLAB(5) DLLM_DLAB(6) DLLM_DLAB(7)
+#undef DLLM_DLAB
+            default: break;
+        }
+    } else if (M <= 16)
         wq_decode_kernel<BITS, YT, 1><<<nb, kDecWaves * 64, 0, st>>>(X, Mi, K, h->wdec, h->sz, h->bias, Y, N, Np, gr);
     else if (M <= 32)
         wq_decode_kernel<BITS, YT, 2><<<nb, kDecWaves * 64, 0, st>>>(X, Mi, K, h->wdec, h->sz, h->bias, Y, N, Np, gr);
@@ -984,7 +1018,11 @@ size_t dllm_linear_weight_bytes(dllm_linear_t h) {
 
 int dllm_linear_set_kernel_variant(dllm_linear_t h, int variant) {
     if (!h) return fail(DLLM_ERR_INVALID_PARAMS, "null handle");
-    if (variant < 0 || variant > 5) return fail(DLLM_ERR_INVALID_PARAMS, "variant must be 0..5");
+    if (variant >= 16 && variant < 24) {   // decode ablation mask (measurement only)
+        h->dlab = variant - 16;
+        return DLLM_OK;
+    }
+    if (variant < 0 || variant > 5) return fail(DLLM_ERR_INVALID_PARAMS, "variant must be 0..5 (16..23: decode ablation)");
     h->variant = variant;
     return DLLM_OK;
 }

@@ -3,7 +3,7 @@ HBM section: FETCH_SIZE reads 1/2 of a wide coalesced stream on gfx950 -> double
 exact for 16-B stores; both in KiB).  Writes profiles/<tag>_pmc_gemm.json."""
 import csv, glob, json, statistics, sys
 root, out = sys.argv[1], sys.argv[2]
-regex = sys.argv[3] if len(sys.argv) > 3 else "wq_gemm_kernel<4, __half"
+regex = sys.argv[3] if len(sys.argv) > 3 else "wq_gemm8_kernel<4,"
 vals = {}
 for f in glob.glob(f"{root}/**/pmc_counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
