@@ -19,6 +19,7 @@
 #include "common.hpp"
 
 #include <algorithm>
+#include <map>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -44,6 +45,7 @@ struct dllm_linear {
     size_t xws_elems = 0;
     int variant = 4;              // prefill schedule variant (tuning knob, see wq_gemm_kernel)
     int dlab = 0;                 // decode-kernel ablation mask (measurement only; 0 in production)
+    int rlab = 0;                 // ring-kernel ablation mask (measurement only; 0 in production)
     std::mutex mu;
 };
 
@@ -273,9 +275,9 @@ constexpr int kMReps = kBM / 32;   // 8
 // | sz [4 waves][64 lanes] u32.  Everything arrives by global_load_lds, so hipcc's counters see no
 // register-destination global load in the loop (mixing the two kinds makes it wait vmcnt(0) at
 // the first use of a register load, which serialised prefetch and compute in the first version).
-template <int BITS>
+template <int BITS, int MR = kMReps>
 struct StageLayout {
-    static constexpr int kX = kBM * kBK * 2;
+    static constexpr int kX = 32 * MR * kBK * 2;
     static constexpr int kW = 4 * 64 * BITS * 4;
     static constexpr int kSZ = 4 * 64 * 4;
     static constexpr int kBytes = kX + kW + kSZ;
@@ -311,12 +313,16 @@ __device__ __forceinline__ void lds_words(uint32_t (&w)[BITS], const uint8_t *wb
     }
 }
 
-template <int BITS, typename YT, int VAR>
-__global__ void __launch_bounds__(kThreads, 2)
+// MR: 32-row m-reps per wave (block tile 32*MR x 128).  SPLIT: the block covers K-slice ks of
+// nsplit and writes its fp32 partial tile to ws[ks][M][Npad] (no bias); splitk_reduce_kernel sums
+// the slices in slice order and applies the bias (deterministic, no atomics).
+template <int BITS, typename YT, int VAR, int MR = kMReps, bool SPLIT = false>
+__global__ void __launch_bounds__(kThreads, (BITS == 8 && MR == 8) ? 1 : 2)
 wq_gemm_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdev,
                const uint32_t *__restrict__ sz, const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad,
-               int group, int nbm, int nbn) {
-    using SL = StageLayout<BITS>;
+               int group, int nbm, int nbn, int nsplit = 1, float *__restrict__ ws = nullptr) {
+    using SL = StageLayout<BITS, MR>;
+    constexpr int kBMt = 32 * MR;
     // Two stage arrays (not one array indexed at run time): with distinct objects the compiler
     // can prove the LDS-DMA into one stage does not alias the ds_reads of the other, and does not
     // insert a vmcnt(0) before every fragment read.
@@ -324,44 +330,49 @@ wq_gemm_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__res
     __shared__ __attribute__((aligned(16))) uint8_t smem1[SL::kBytes];
 
     // XCD-aware bijective remap: consecutive logical tiles (same bm row panel of X) share an XCD.
-    const int nb = nbm * nbn, orig = blockIdx.x;
+    // K-slice outermost, so the blocks an XCD holds share the slice's X rows in its L2.
+    const int nb = nbm * nbn * nsplit, orig = blockIdx.x;
     const int xcd = orig % kXCDs, q8 = nb / kXCDs, r8 = nb % kXCDs;
     const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / kXCDs;
-    const int bm = wgid / nbn, bn = wgid % nbn;
+    const int ks = wgid / (nbm * nbn), tile = wgid % (nbm * nbn);
+    const int bm = tile / nbn, bn = tile % nbn;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int m0 = bm * kBM, n0 = bn * kBN;
-    const unsigned nk = static_cast<unsigned>(K) / kBK;
+    const int m0 = bm * kBMt, n0 = bn * kBN;
+    const unsigned nk_all = static_cast<unsigned>(K) / kBK;
+    const unsigned nk = nk_all / static_cast<unsigned>(nsplit);   // k-steps in this slice
+    const unsigned kt0 = static_cast<unsigned>(ks) * nk;
     const unsigned kpg = static_cast<unsigned>(group) / kBK;   // k-steps per quantization group
     const unsigned nt = static_cast<unsigned>(n0 + wave * 32) >> 5;
     const int ncol = n0 + wave * 32 + (lane & 31);
 
     // glds source pointers.
     const int chunk_st = lane & 7;
-    const __half *xsrc[8];
+    const __half *xsrc[MR];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < MR; ++i) {
         const int row = i * 32 + wave * 8 + (lane >> 3);
         int grow = m0 + row;
         grow = grow < M ? grow : M - 1;
         const int c = chunk_st ^ ((row >> 1) & 7);
         xsrc[i] = X + static_cast<size_t>(grow) * K + c * 8;
     }
-    const uint32_t *wsrc = wdev + (static_cast<size_t>(nt) * nk * 64 + lane) * BITS;   // + kt*64*BITS
+    const uint32_t *wsrc = wdev + (static_cast<size_t>(nt) * nk_all * 64 + lane) * BITS;   // + kt*64*BITS
     const uint32_t *szsrc = sz + ncol;                                                  // + g*Npad
 
     auto stage = [&](uint8_t *sb, unsigned kt) {
         uint8_t *xb = sb + wave * 1024;   // 1 KiB per wave-instruction
+        kt += kt0;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) glds16(xsrc[i] + kt * kBK, xb + i * 4096);
+        for (int i = 0; i < MR; ++i) glds16(xsrc[i] + kt * kBK, xb + i * 4096);
         glds_words<BITS>(wsrc + static_cast<size_t>(kt) * 64 * BITS, sb + SL::kX + wave * (64 * BITS * 4));
         __builtin_amdgcn_global_load_lds((gbl_void_ptr)(const_cast<uint32_t *>(szsrc + (kt / kpg) * Npad)),
                                          (lds_void_ptr)(sb + SL::kX + SL::kW + wave * 256), 4, 0, 0);
     };
 
-    float16_t acc[kMReps];
+    float16_t acc[MR];
 #pragma unroll
-    for (int r = 0; r < kMReps; ++r)
+    for (int r = 0; r < MR; ++r)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[r][e] = 0.0f;
 
@@ -378,13 +389,13 @@ wq_gemm_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__res
     // VAR 1: same data flow, compiler-scheduled; VAR 2: A and B fragments both one substep ahead,
     // MFMAs interleaved with the next substep's ds_reads and dequant VALU by sched_group_barrier;
     // VAR 3: VAR 2 + s_setprio(1) around each MFMA group.
-    auto read_b = [&](half8_t (&b)[kMReps], const uint8_t *sb, int s) {
+    auto read_b = [&](half8_t (&b)[MR], const uint8_t *sb, int s) {
 #pragma unroll
-        for (int r = 0; r < kMReps; ++r) b[r] = *reinterpret_cast<const half8_t *>(sb + soff[s] + r * 32 * kBK * 2);
+        for (int r = 0; r < MR; ++r) b[r] = *reinterpret_cast<const half8_t *>(sb + soff[s] + r * 32 * kBK * 2);
     };
-    auto mfma8 = [&](const half8_t &a, const half8_t (&b)[kMReps]) {
+    auto mfma8 = [&](const half8_t &a, const half8_t (&b)[MR]) {
 #pragma unroll
-        for (int r = 0; r < kMReps; ++r) acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b[r], acc[r], 0, 0, 0);
+        for (int r = 0; r < MR; ++r) acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b[r], acc[r], 0, 0, 0);
     };
     auto step = [&](const uint8_t *sb, uint8_t *nb_, unsigned kt) {
         if (kt + 1 < nk) stage(nb_, kt + 1);
@@ -392,7 +403,7 @@ wq_gemm_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__res
         lds_words<BITS>(w, sb + SL::kX + wave * (64 * BITS * 4), lane);
         half2_t nz, sc;
         split_sz(*reinterpret_cast<const uint32_t *>(sb + SL::kX + SL::kW + wave * 256 + lane * 4), nz, sc);
-        half8_t bA[kMReps], bB[kMReps];
+        half8_t bA[MR], bB[MR];
         read_b(bA, sb, 0);
         if constexpr (VAR <= 1) {
 #pragma unroll
@@ -408,7 +419,7 @@ wq_gemm_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__res
             }
         } else {
             half8_t aA = dequant_frag<BITS>(w, 0, nz, sc), aB;
-            auto sub = [&](half8_t (&bc)[kMReps], half8_t (&bn)[kMReps], const half8_t &ac, half8_t &an, int s) {
+            auto sub = [&](half8_t (&bc)[MR], half8_t (&bn)[MR], const half8_t &ac, half8_t &an, int s) {
                 __builtin_amdgcn_sched_barrier(0);
                 if constexpr (VAR == 3) __builtin_amdgcn_s_setprio(1);
                 if (s < 3) {
@@ -417,7 +428,7 @@ wq_gemm_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__res
                 }
                 mfma8(ac, bc);
 #pragma unroll
-                for (int i = 0; i < kMReps; ++i) {
+                for (int i = 0; i < MR; ++i) {
                     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
                     __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
                     __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);   // VALU
@@ -444,13 +455,28 @@ wq_gemm_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__res
 
     // Epilogue: acc[r] reg e -> n = n0 + 32*wave + (e&3) + 8*(e>>2) + 4*hsel, m = m0 + 32r + (lane&31).
     const int nb0 = n0 + wave * 32 + 4 * hsel;
+    if constexpr (SPLIT) {
+        // Partial tile (rows < M, all Npad columns exist in the slab): 16-B stores, no bias.
+        float *slab = ws + static_cast<size_t>(ks) * M * Npad;
+#pragma unroll
+        for (int r = 0; r < MR; ++r) {
+            const int m = m0 + r * 32 + (lane & 31);
+            if (m >= M) continue;
+            float *prow = slab + static_cast<size_t>(m) * Npad + nb0;
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd)
+                *reinterpret_cast<float4 *>(prow + 8 * qd) =
+                    make_float4(acc[r][4 * qd + 0], acc[r][4 * qd + 1], acc[r][4 * qd + 2], acc[r][4 * qd + 3]);
+        }
+        return;
+    }
     float4 bv[4];
 #pragma unroll
     for (int qd = 0; qd < 4; ++qd) bv[qd] = *reinterpret_cast<const float4 *>(bias + nb0 + 8 * qd);
-    const bool full = (m0 + kBM <= M) && (n0 + kBN <= N) && (N % 4) == 0;
+    const bool full = (m0 + kBMt <= M) && (n0 + kBN <= N) && (N % 4) == 0;
     if (full) {
 #pragma unroll
-        for (int r = 0; r < kMReps; ++r) {
+        for (int r = 0; r < MR; ++r) {
             YT *yrow = Y + static_cast<size_t>(m0 + r * 32 + (lane & 31)) * N + nb0;
 #pragma unroll
             for (int qd = 0; qd < 4; ++qd)
@@ -460,7 +486,7 @@ wq_gemm_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__res
     } else {
         const bool vec_ok = (N % 4) == 0;
 #pragma unroll
-        for (int r = 0; r < kMReps; ++r) {
+        for (int r = 0; r < MR; ++r) {
             const int m = m0 + r * 32 + (lane & 31);
             if (m >= M) continue;
             YT *yrow = Y + static_cast<size_t>(m) * N;
@@ -495,114 +521,164 @@ __device__ __forceinline__ void glds4_asm(const void *gsrc, uint32_t lds_dst) {
                  : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
 }
 
-constexpr int kBN8 = 256;
 
-template <int BITS>
+template <int BITS, int NW = 8, int MR = kMReps, int KG = 1>
 struct StageLayout8 {
-    static constexpr int kX = kBM * kBK * 2;            // 32 KiB
-    static constexpr int kW = 8 * 64 * BITS * 4;        // 8 waves
-    static constexpr int kSZ = 8 * 64 * 4;
+    static constexpr int kWaves = NW * KG;
+    static constexpr int kXRounds = 4 * MR / kWaves;      // 1-KiB wave-instructions per wave for X
+    static constexpr int kX = 32 * MR * kBK * 2;
+    static constexpr int kW = NW * 64 * BITS * 4;
+    static constexpr int kSZ = NW * 64 * 4;
     static constexpr int kBytes = kX + kW + kSZ;
-    // LDS-DMA instructions per wave per stage: 4 X rounds + weight words + 1 scale dword.
-    static constexpr int kOps = 4 + (BITS == 4 ? 1 : 2) + 1;
+    static constexpr int kWOps = BITS == 4 ? 1 : 2;
+    // LDS-DMA instructions per wave per stage.  KG = 1: X rounds + weight words + 1 scale dword.
+    // KG = 2: k-group 0 loads the weight words, k-group 1 the scales.
+    static constexpr int kOps0 = kXRounds + kWOps + (KG == 1 ? 1 : 0);
+    static constexpr int kOps1 = kXRounds + 1;
 };
 
-template <int BITS, typename YT>
-__global__ void __launch_bounds__(512, 1)
+// Ring GEMM: block tile (32 MR) x (32 NW), NW*KG waves.  Wave (cw, kg) = (wave % NW, wave / NW)
+// owns output columns n0 + 32 cw .. +32 for all 32 MR rows and, of every 64-deep k-step, the
+// 4/KG substeps kg*4/KG ..: KG = 2 puts two waves on each SIMD at the same tile count (the 128-row
+// tiles of mid-M shapes run one block per CU), their two accumulators summed through the stage
+// LDS at the end (fixed order).  SPLIT: as wq_gemm_kernel (slab partial, no bias).
+template <int BITS, typename YT, int NW = 8, int MR = kMReps, bool SPLIT = false, int KG = 1, int LAB = 0>
+__global__ void __launch_bounds__(NW * KG * 64, (NW * KG == 8 || MR == 8) ? 1 : 2)
 wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdev,
                 const uint32_t *__restrict__ sz, const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad,
-                int group, int nbm, int nbn) {
-    using SL = StageLayout8<BITS>;
+                int group, int nbm, int nbn, int nsplit = 1, float *__restrict__ ws = nullptr) {
+    using SL = StageLayout8<BITS, NW, MR, KG>;
+    constexpr int kBMt = 32 * MR, kBNt = 32 * NW, kWT = NW * KG, kSub = 4 / KG;
+    static_assert(SL::kXRounds >= 1 && 4 * MR % kWT == 0, "X staging must split evenly over the waves");
     __shared__ __attribute__((aligned(16))) uint8_t st0[SL::kBytes];
     __shared__ __attribute__((aligned(16))) uint8_t st1[SL::kBytes];
     __shared__ __attribute__((aligned(16))) uint8_t st2[SL::kBytes];
 
-    const int nb = nbm * nbn, orig = blockIdx.x;
+    // K-slice outermost, so the blocks an XCD holds share the slice's X rows in its L2.
+    const int nb = nbm * nbn * nsplit, orig = blockIdx.x;
     const int xcd = orig % kXCDs, q8 = nb / kXCDs, r8 = nb % kXCDs;
     const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / kXCDs;
-    const int bm = wgid / nbn, bn = wgid % nbn;
+    const int ks = wgid / (nbm * nbn), tile = wgid % (nbm * nbn);
+    const int bm = tile / nbn, bn = tile % nbn;
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int m0 = bm * kBM, n0 = bn * kBN8;
-    const unsigned nk = static_cast<unsigned>(K) / kBK;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int cw = wave % NW, kg = wave / NW;
+    const int m0 = bm * kBMt, n0 = bn * kBNt;
+    const unsigned nk_all = static_cast<unsigned>(K) / kBK;
+    const unsigned nk = nk_all / static_cast<unsigned>(nsplit);   // k-steps of this K slice
+    const unsigned kt0 = static_cast<unsigned>(ks) * nk;
     const unsigned kpg = static_cast<unsigned>(group) / kBK;
-    const unsigned nt = static_cast<unsigned>(n0 + wave * 32) >> 5;
-    const int ncol = n0 + wave * 32 + (lane & 31);
+    const unsigned nt = static_cast<unsigned>(n0 + cw * 32) >> 5;
+    const int ncol = n0 + cw * 32 + (lane & 31);
 
-    // X: 4 rounds x 8 KiB (512 threads x 16 B); round i, wave w covers rows 64 i + 8 w .. +8.
+    // X: kXRounds rounds of kWT KiB (kWT waves x 64 lanes x 16 B); round i, wave w covers rows
+    // 8 (kWT i + w) .. +8.
     const int chunk_st = lane & 7;
-    const __half *xsrc[4];
+    const __half *xsrc[SL::kXRounds];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int row = i * 64 + wave * 8 + (lane >> 3);
+    for (int i = 0; i < SL::kXRounds; ++i) {
+        const int row = (i * kWT + wave) * 8 + (lane >> 3);
         int grow = m0 + row;
         grow = grow < M ? grow : M - 1;
         const int c = chunk_st ^ ((row >> 1) & 7);
         xsrc[i] = X + static_cast<size_t>(grow) * K + c * 8;
     }
-    const uint32_t *wsrc = wdev + (static_cast<size_t>(nt) * nk * 64 + lane) * BITS;
+    const uint32_t *wsrc = wdev + (static_cast<size_t>(nt) * nk_all * 64 + lane) * BITS;
     const uint32_t *szsrc = sz + ncol;
 
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(wave);
-    auto stage = [&](uint8_t *sb, unsigned kt) {
+    const uint32_t wv = static_cast<uint32_t>(wave), cwv = static_cast<uint32_t>(cw);
+    // A stage is kXRounds + 2 pieces: X rounds, the weight words, the scale dword (pieces a wave
+    // does not own under KG = 2 are empty), issued as one burst at the top of a k-step.  Spreading
+    // the pieces over the substeps (to hide each DMA's issue cost) measured slower: the later
+    // issue shortens the landing slack before the counted wait two steps on.
+    constexpr int kPieces = SL::kXRounds + 2;
+    auto piece = [&](uint8_t *sb, unsigned kt, int p) {
         const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(sb));
-#pragma unroll
-        for (int i = 0; i < 4; ++i) glds16_asm(xsrc[i] + kt * kBK, base + wv * 1024 + i * 8192);
-        const uint32_t *wp = wsrc + static_cast<size_t>(kt) * 64 * BITS;
-        const uint32_t wb = base + SL::kX + wv * (64 * BITS * 4);
-        if constexpr (BITS == 4) {
-            glds16_asm(wp, wb);
-        } else if constexpr (BITS == 8) {
-            glds16_asm(wp, wb);
-            glds16_asm(wp + 4, wb + 64 * 16);
-        } else {
-            glds4_asm(wp, wb);
-            glds4_asm(wp + 1, wb + 256);
+        kt += kt0;
+        if (p < SL::kXRounds) {
+            if constexpr (!(LAB & 1)) glds16_asm(xsrc[p] + kt * kBK, base + wv * 1024 + p * kWT * 1024);
+            return;
         }
-        glds4_asm(szsrc + (kt / kpg) * Npad, base + SL::kX + SL::kW + wv * 256);
+        if constexpr (LAB & 2) return;
+        if (p == SL::kXRounds) {
+            if (KG == 1 || kg == 0) {
+                const uint32_t *wp = wsrc + static_cast<size_t>(kt) * 64 * BITS;
+                const uint32_t wb = base + SL::kX + cwv * (64 * BITS * 4);
+                if constexpr (BITS == 4) {
+                    glds16_asm(wp, wb);
+                } else if constexpr (BITS == 8) {
+                    glds16_asm(wp, wb);
+                    glds16_asm(wp + 4, wb + 64 * 16);
+                } else {
+                    glds4_asm(wp, wb);
+                    glds4_asm(wp + 1, wb + 256);
+                }
+            }
+        } else if (KG == 1 || kg == 1) {
+            glds4_asm(szsrc + (kt / kpg) * Npad, base + SL::kX + SL::kW + cwv * 256);
+        }
+    };
+    auto stage = [&](uint8_t *sb, unsigned kt) {
+#pragma unroll
+        for (int p = 0; p < kPieces; ++p) piece(sb, kt, p);
+    };
+    // Counted wait leaving the newest stage's DMAs (this wave's own count) in flight.
+    auto wait_prev = [&]() {
+        if (KG == 1 || kg == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kOps0) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kOps1) : "memory");
     };
 
-    float16_t acc[kMReps];
+    float16_t acc[MR];
 #pragma unroll
-    for (int r = 0; r < kMReps; ++r)
+    for (int r = 0; r < MR; ++r)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[r][e] = 0.0f;
 
     const int hsel = lane >> 5;
     const int rowx = ((lane & 31) >> 1) & 7;
-    int soff[4];
+    // This wave's substeps: kg * kSub + j, j < kSub (fragment offsets selected once, uniform).
+    int soff[kSub];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) soff[s] = (lane & 31) * (kBK * 2) + ((((2 * s + hsel) ^ rowx)) << 4);
+    for (int j = 0; j < kSub; ++j) {
+        const int s = kg * kSub + j;
+        soff[j] = (lane & 31) * (kBK * 2) + ((((2 * s + hsel) ^ rowx)) << 4);
+    }
 
-    auto read_b = [&](half8_t (&b)[kMReps], const uint8_t *sb, int s) {
+    auto read_b = [&](half8_t (&b)[MR], const uint8_t *sb, int j) {
 #pragma unroll
-        for (int r = 0; r < kMReps; ++r) b[r] = *reinterpret_cast<const half8_t *>(sb + soff[s] + r * 32 * kBK * 2);
+        for (int r = 0; r < MR; ++r) b[r] = *reinterpret_cast<const half8_t *>(sb + soff[j] + r * 32 * kBK * 2);
     };
-    auto mfma8 = [&](const half8_t &a, const half8_t (&b)[kMReps]) {
+    auto mfma8 = [&](const half8_t &a, const half8_t (&b)[MR]) {
 #pragma unroll
-        for (int r = 0; r < kMReps; ++r) acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b[r], acc[r], 0, 0, 0);
+        for (int r = 0; r < MR; ++r) acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b[r], acc[r], 0, 0, 0);
     };
     // Compute stage `sb`; stage `pf` receives k-step kt+2.
     auto step = [&](const uint8_t *sb, uint8_t *pf, unsigned kt) {
         const bool issue = kt + 2 < nk;
         if (issue) stage(pf, kt + 2);
         uint32_t w[BITS];
-        lds_words<BITS>(w, sb + SL::kX + wave * (64 * BITS * 4), lane);
+        lds_words<BITS>(w, sb + SL::kX + cw * (64 * BITS * 4), lane);
+        if constexpr (KG == 2) {
+            // Substeps 2 kg + j of the slab words = substeps j of the words shifted by kg * BITS/2.
+#pragma unroll
+            for (int i = 0; i < BITS / 2; ++i) w[i] = kg ? w[BITS / 2 + i] : w[i];
+        }
         half2_t nz, sc;
-        split_sz(*reinterpret_cast<const uint32_t *>(sb + SL::kX + SL::kW + wave * 256 + lane * 4), nz, sc);
-        half8_t bA[kMReps], bB[kMReps];
+        split_sz(*reinterpret_cast<const uint32_t *>(sb + SL::kX + SL::kW + cw * 256 + lane * 4), nz, sc);
+        half8_t bA[MR], bB[MR];
         read_b(bA, sb, 0);
         half8_t aA = dequant_frag<BITS>(w, 0, nz, sc), aB;
-        auto sub = [&](half8_t (&bc)[kMReps], half8_t (&bn)[kMReps], const half8_t &ac, half8_t &an, int s) {
+        auto sub = [&](half8_t (&bc)[MR], half8_t (&bn)[MR], const half8_t &ac, half8_t &an, int j) {
             __builtin_amdgcn_sched_barrier(0);
             __builtin_amdgcn_s_setprio(1);
-            if (s < 3) {
-                read_b(bn, sb, s + 1);
-                an = dequant_frag<BITS>(w, s + 1, nz, sc);
+            if (j < kSub - 1) {
+                read_b(bn, sb, j + 1);
+                an = dequant_frag<BITS>(w, j + 1, nz, sc);
             }
             mfma8(ac, bc);
 #pragma unroll
-            for (int i = 0; i < kMReps; ++i) {
+            for (int i = 0; i < MR; ++i) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
                 __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                 __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
@@ -612,10 +688,12 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
         };
         sub(bA, bB, aA, aB, 0);
         sub(bB, bA, aB, aA, 1);
-        sub(bA, bB, aA, aB, 2);
-        sub(bB, bA, aB, aA, 3);
+        if constexpr (kSub == 4) {
+            sub(bA, bB, aA, aB, 2);
+            sub(bB, bA, aB, aA, 3);
+        }
         // Stage kt+1 must have landed; kt+2's DMAs may stay in flight across the barrier.
-        if (issue) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kOps) : "memory");
+        if (issue) wait_prev();
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
@@ -624,7 +702,7 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
 
     stage(st0, 0);
     if (nk > 1) stage(st1, 1);
-    if (nk > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kOps) : "memory");
+    if (nk > 1) wait_prev();
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -634,14 +712,66 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
         if (kt + 2 < nk) step(st2, st1, kt + 2);
     }
 
-    const int nb0 = n0 + wave * 32 + 4 * hsel;
+    if constexpr (KG == 2) {
+        // k-group 1 hands its accumulators to k-group 0 through the (now idle) stage buffers,
+        // three m-reps per pass (one 16-KiB rep image per stage array), float4-lane-linear.
+        static_assert(NW * 64 * 16 * 4 <= SL::kBytes, "a rep image must fit one stage array");
+        uint8_t *bufs[3] = {st0, st1, st2};
+#pragma unroll
+        for (int r0 = 0; r0 < MR; r0 += 3) {
+            if (kg == 1) {
+#pragma unroll
+                for (int u = 0; u < 3; ++u) {
+                    if (r0 + u >= MR) break;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        *reinterpret_cast<float4 *>(bufs[u] + ((q * NW + cw) * 64 + lane) * 16) =
+                            make_float4(acc[r0 + u][4 * q], acc[r0 + u][4 * q + 1], acc[r0 + u][4 * q + 2],
+                                        acc[r0 + u][4 * q + 3]);
+                }
+            }
+            __syncthreads();
+            if (kg == 0) {
+#pragma unroll
+                for (int u = 0; u < 3; ++u) {
+                    if (r0 + u >= MR) break;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const float4 o = *reinterpret_cast<const float4 *>(bufs[u] + ((q * NW + cw) * 64 + lane) * 16);
+                        acc[r0 + u][4 * q] += o.x;
+                        acc[r0 + u][4 * q + 1] += o.y;
+                        acc[r0 + u][4 * q + 2] += o.z;
+                        acc[r0 + u][4 * q + 3] += o.w;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        if (kg != 0) return;
+    }
+
+    const int nb0 = n0 + cw * 32 + 4 * hsel;
+    if constexpr (SPLIT) {
+        float *slab = ws + static_cast<size_t>(ks) * M * Npad;
+#pragma unroll
+        for (int r = 0; r < MR; ++r) {
+            const int m = m0 + r * 32 + (lane & 31);
+            if (m >= M) continue;
+            float *prow = slab + static_cast<size_t>(m) * Npad + nb0;
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd)
+                *reinterpret_cast<float4 *>(prow + 8 * qd) =
+                    make_float4(acc[r][4 * qd + 0], acc[r][4 * qd + 1], acc[r][4 * qd + 2], acc[r][4 * qd + 3]);
+        }
+        return;
+    }
     float4 bv[4];
 #pragma unroll
     for (int qd = 0; qd < 4; ++qd) bv[qd] = *reinterpret_cast<const float4 *>(bias + nb0 + 8 * qd);
-    const bool full = (m0 + kBM <= M) && (n0 + kBN8 <= N) && (N % 4) == 0;
+    const bool full = (m0 + kBMt <= M) && (n0 + kBNt <= N) && (N % 4) == 0;
     if (full) {
 #pragma unroll
-        for (int r = 0; r < kMReps; ++r) {
+        for (int r = 0; r < MR; ++r) {
             YT *yrow = Y + static_cast<size_t>(m0 + r * 32 + (lane & 31)) * N + nb0;
 #pragma unroll
             for (int qd = 0; qd < 4; ++qd)
@@ -651,7 +781,7 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
     } else {
         const bool vec_ok = (N % 4) == 0;
 #pragma unroll
-        for (int r = 0; r < kMReps; ++r) {
+        for (int r = 0; r < MR; ++r) {
             const int m = m0 + r * 32 + (lane & 31);
             if (m >= M) continue;
             YT *yrow = Y + static_cast<size_t>(m) * N;
@@ -822,21 +952,153 @@ void launch_prefill(const dllm_linear *h, const __half *X, int M, YT *Y, hipStre
                                                            (int)h->Npad, (int)h->group, nbm, nbn);
 }
 
+// Split-K combine: Y[m][n] = sum_s ws[s][m][n] (slice order) + bias[n]; 4 outputs per thread.
+template <typename YT>
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const float *__restrict__ ws, int nsplit, int M, int N,
+                                                            int Npad, const float *__restrict__ bias,
+                                                            YT *__restrict__ Y) {
+    const int q = Npad / 4;
+    const size_t total = static_cast<size_t>(M) * q, slab = static_cast<size_t>(M) * Npad;
+    const bool vec_ok = (N % 4) == 0;
+    for (size_t i = blockIdx.x * static_cast<size_t>(256) + threadIdx.x; i < total;
+         i += static_cast<size_t>(gridDim.x) * 256) {
+        const int m = static_cast<int>(i / q), n = static_cast<int>(i % q) * 4;
+        if (n >= N) continue;
+        const float *p = ws + static_cast<size_t>(m) * Npad + n;
+        float4 a = *reinterpret_cast<const float4 *>(p);
+        for (int s = 1; s < nsplit; ++s) {
+            const float4 b = *reinterpret_cast<const float4 *>(p + s * slab);
+            a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+        }
+        store_out4<YT>(Y + static_cast<size_t>(m) * N, bias, n, N, vec_ok, a.x, a.y, a.z, a.w);
+    }
+}
+
+// Split-K slab workspace, one per (device, stream): launches on one stream run in order, so every
+// layer on that stream can share it.  It only grows; a growth waits for the stream first (queued
+// kernels may still read the old one) and is refused while the stream is being captured.
+float *splitk_workspace(hipStream_t st, size_t bytes) {
+    static std::mutex mu;
+    static std::map<std::pair<int, hipStream_t>, std::pair<float *, size_t>> pool;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(mu);
+    auto &e = pool[{dev, st}];
+    if (e.second >= bytes) return e.first;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(st, &cs);
+    if (cs != hipStreamCaptureStatusNone) {
+        fail(DLLM_ERR_HIP, "split-K workspace must be sized before stream capture (run the shape once first)");
+        return nullptr;
+    }
+    if (e.first) {
+        if (hipStreamSynchronize(st) != hipSuccess) return nullptr;
+        (void)hipFree(e.first);
+        e = {nullptr, 0};
+    }
+    float *p = nullptr;
+    if (hipMalloc(reinterpret_cast<void **>(&p), bytes) != hipSuccess) {
+        fail(DLLM_ERR_HIP, "hipMalloc of the split-K workspace failed");
+        return nullptr;
+    }
+    e = {p, bytes};
+    return p;
+}
+
+// Mid-M prefill (too few 256-row tiles to fill 256 CUs): 128-row tiles, and when even those are
+// too few, K split into nsplit slices (slab partials + splitk_reduce_kernel).
+template <int BITS, typename YT>
+int launch_mid(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t st) {
+    constexpr int MR = 4;
+    const int nbm = (M + 32 * MR - 1) / (32 * MR), nbn = static_cast<int>(h->Npad / kBN);
+    const int tiles = nbm * nbn;
+    const int nk = static_cast<int>(h->K / kBK);
+    int nsplit = 1;
+    while (tiles * nsplit < 200 && nsplit < 8 && nk % (2 * nsplit) == 0 && nk / (2 * nsplit) >= 4) nsplit *= 2;
+    const unsigned nb = static_cast<unsigned>(tiles * nsplit);
+    if (nsplit == 1) {
+        wq_gemm_kernel<BITS, YT, 3, MR, false><<<nb, kThreads, 0, st>>>(
+            X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn);
+        DLLM_LAUNCH_CHECK();
+        return DLLM_OK;
+    }
+    float *ws = splitk_workspace(st, static_cast<size_t>(nsplit) * M * h->Npad * sizeof(float));
+    if (!ws) return DLLM_ERR_HIP;
+    wq_gemm_kernel<BITS, YT, 3, MR, true><<<nb, kThreads, 0, st>>>(
+        X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn, nsplit, ws);
+    DLLM_LAUNCH_CHECK();
+    const size_t q = static_cast<size_t>(M) * (h->Npad / 4);
+    const unsigned rb = static_cast<unsigned>(std::min<size_t>((q + 255) / 256, 4 * kCUs));
+    splitk_reduce_kernel<YT><<<rb, 256, 0, st>>>(ws, nsplit, M, (int)h->N, (int)h->Npad, h->bias, Y);
+    DLLM_LAUNCH_CHECK();
+    return DLLM_OK;
+}
+
+// 3-stage-ring GEMM with tile (32 MR) x (32 NW), K optionally split into nsplit slices.
+template <int BITS, typename YT, int NW, int MR, int KG = 1>
+int launch_ring(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t st, int nsplit) {
+    const int nbm = (M + 32 * MR - 1) / (32 * MR), nbn = static_cast<int>(h->Npad / (32 * NW));
+    const unsigned nb = static_cast<unsigned>(nbm * nbn * nsplit);
+    if (h->rlab != 0 && nsplit == 1) {   // measurement only
+        if (h->rlab == 1)
+            wq_gemm8_kernel<BITS, YT, NW, MR, false, KG, 1><<<nb, NW * KG * 64, 0, st>>>(
+                X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn);
+        else if (h->rlab == 2)
+            wq_gemm8_kernel<BITS, YT, NW, MR, false, KG, 2><<<nb, NW * KG * 64, 0, st>>>(
+                X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn);
+        else
+            wq_gemm8_kernel<BITS, YT, NW, MR, false, KG, 3><<<nb, NW * KG * 64, 0, st>>>(
+                X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn);
+        DLLM_LAUNCH_CHECK();
+        return DLLM_OK;
+    }
+    if (nsplit == 1) {
+        wq_gemm8_kernel<BITS, YT, NW, MR, false, KG><<<nb, NW * KG * 64, 0, st>>>(
+            X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn);
+        DLLM_LAUNCH_CHECK();
+        return DLLM_OK;
+    }
+    float *ws = splitk_workspace(st, static_cast<size_t>(nsplit) * M * h->Npad * sizeof(float));
+    if (!ws) return DLLM_ERR_HIP;
+    wq_gemm8_kernel<BITS, YT, NW, MR, true, KG><<<nb, NW * KG * 64, 0, st>>>(
+        X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn, nsplit, ws);
+    DLLM_LAUNCH_CHECK();
+    const size_t q = static_cast<size_t>(M) * (h->Npad / 4);
+    const unsigned rb = static_cast<unsigned>(std::min<size_t>((q + 255) / 256, 4 * kCUs));
+    splitk_reduce_kernel<YT><<<rb, 256, 0, st>>>(ws, nsplit, M, (int)h->N, (int)h->Npad, h->bias, Y);
+    DLLM_LAUNCH_CHECK();
+    return DLLM_OK;
+}
+
+// Tile policy (variant 4, the default): the largest tile that still gives >= 256 blocks; below
+// that, 128 x 128 tiles with K split until ~200+ blocks (slab partials + ordered combine).
+template <int BITS, typename YT>
+int launch_auto(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t st) {
+    const int np = static_cast<int>(h->Npad);
+    const int mb256 = (M + 255) / 256, mb128 = (M + 127) / 128;
+    if (np % 256 == 0 && mb256 * (np / 256) >= kCUs) return launch_ring<BITS, YT, 8, 8>(h, X, M, Y, st, 1);
+    const bool kg2 = h->variant == 4;   // variant 5: the same tiles with one k-group (A/B)
+    if (mb256 * (np / 128) >= kCUs)
+        return kg2 ? launch_ring<BITS, YT, 4, 8, 2>(h, X, M, Y, st, 1) : launch_ring<BITS, YT, 4, 8, 1>(h, X, M, Y, st, 1);
+    const int tiles = mb128 * (np / 128);
+    const int nk = static_cast<int>(h->K / kBK);
+    int nsplit = 1;
+    while (tiles * nsplit < 200 && nsplit < 8 && nk % (2 * nsplit) == 0 && nk / (2 * nsplit) >= 4) nsplit *= 2;
+    return kg2 ? launch_ring<BITS, YT, 4, 4, 2>(h, X, M, Y, st, nsplit)
+               : launch_ring<BITS, YT, 4, 4, 1>(h, X, M, Y, st, nsplit);
+}
+
 template <int BITS, typename YT>
 int launch_gemm_t(const dllm_linear *h, const __half *X, size_t M, YT *Y, hipStream_t st) {
     if (M <= static_cast<size_t>(kDecodeMaxM)) return launch_decode<BITS, YT>(h, X, M, Y, st);
-    const int nbm8 = static_cast<int>((M + kBM - 1) / kBM), nbn8 = static_cast<int>((h->Npad + kBN8 - 1) / kBN8);
-    const bool big_ok = (h->Npad % kBN8) == 0 && nbm8 * nbn8 >= kCUs;
-    if ((h->variant == 4 || h->variant == 5) && big_ok) {
-        wq_gemm8_kernel<BITS, YT><<<static_cast<unsigned>(nbm8 * nbn8), 512, 0, st>>>(
-            X, (int)M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm8, nbn8);
-        DLLM_LAUNCH_CHECK();
-        return DLLM_OK;
+    if (h->variant == 4 || h->variant == 5) return launch_auto<BITS, YT>(h, X, (int)M, Y, st);
+    if (h->variant == 6) {   // previous policy: 2-stage kernels, 128-row tiles + split below 256 tiles
+        const int tiles256 = static_cast<int>((M + kBM - 1) / kBM) * static_cast<int>(h->Npad / kBN);
+        if (tiles256 < kCUs) return launch_mid<BITS, YT>(h, X, (int)M, Y, st);
     }
     switch (h->variant) {
     case 0: launch_prefill<BITS, YT, 0>(h, X, (int)M, Y, st); break;
     case 1: launch_prefill<BITS, YT, 1>(h, X, (int)M, Y, st); break;
-
     case 2: launch_prefill<BITS, YT, 2>(h, X, (int)M, Y, st); break;
     default: launch_prefill<BITS, YT, 3>(h, X, (int)M, Y, st); break;
     }
@@ -1022,8 +1284,13 @@ int dllm_linear_set_kernel_variant(dllm_linear_t h, int variant) {
         h->dlab = variant - 16;
         return DLLM_OK;
     }
-    if (variant < 0 || variant > 5) return fail(DLLM_ERR_INVALID_PARAMS, "variant must be 0..5 (16..23: decode ablation)");
+    if (variant >= 32 && variant < 36) {   // ring-kernel ablation mask (measurement only)
+        h->rlab = variant - 32;
+        return DLLM_OK;
+    }
+    if (variant < 0 || variant > 6) return fail(DLLM_ERR_INVALID_PARAMS, "variant must be 0..6 (16..23: decode ablation)");
     h->variant = variant;
+    h->dlab = h->rlab = 0;
     return DLLM_OK;
 }
 

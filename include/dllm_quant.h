@@ -10,7 +10,8 @@
  *     DLLM_ERR_INVALID_PARAMS; 16+ = HIP / runtime errors.  dllm_last_error() gives a message.
  *   - plain pointers and sizes only.  Unless a name ends in _host, every data pointer is DEVICE
  *     memory and the call is asynchronous on `stream` (a hipStream_t; NULL = default stream);
- *     nothing is allocated or synchronised inside (graph-capturable).  The *_host variants take
+ *     nothing is synchronised inside and, after a first call of the same shape, nothing is
+ *     allocated (graph-capturable; see dllm_linear_forward).  The *_host variants take
  *     host pointers, stage through device memory and synchronise (parity/test convenience).
  *   - quantized codes are either one code per byte ("unpacked", the reference's storage,
  *     diffuse-llm-rs/src/quantization.rs:59-65) or the packed LSB-first bitstream below.
@@ -151,8 +152,11 @@ int dllm_linear_create(const float *W, const float *bias, size_t K, size_t N, ui
 int dllm_linear_create_quantized(const uint8_t *packed_codes, const float *scales, const uint8_t *zps,
                                  const float *bias, size_t K, size_t N, uint8_t bits, size_t group,
                                  dllm_linear_t *out, dllm_stream_t stream);
-/* Y[M][ldy] = X[M][K] . W^ + b.  x_dtype/y_dtype in {DLLM_F32, DLLM_F16}; an f32 X is cast to f16
- * through a workspace owned by the handle (grown outside stream capture, before the launch). */
+/* Y[M][N] = X[M][K] . W^ + b.  x_dtype/y_dtype in {DLLM_F32, DLLM_F16}; an f32 X is cast to f16
+ * through a workspace owned by the handle.  Shapes with too few output tiles to fill the GPU
+ * (M roughly 65..1000 at N = 4096) split K into slices whose f32 partials are combined in slice
+ * order (deterministic) through a per-(device, stream) workspace.  Both workspaces only grow and
+ * are allocated on the first call that needs them, which therefore must precede stream capture. */
 int dllm_linear_forward(dllm_linear_t h, const void *X, size_t M, int x_dtype, void *Y, int y_dtype,
                         dllm_stream_t stream);
 /* Export the quantized weights in canonical form (packed bitstream [K][N], scales [G][N], zps). */
@@ -161,7 +165,10 @@ int dllm_linear_export(dllm_linear_t h, uint8_t *packed_codes, float *scales, ui
 int dllm_linear_info(dllm_linear_t h, size_t *K, size_t *N, uint8_t *bits, size_t *group);
 /* HBM bytes the forward's GEMM kernel reads for the weights (packed codes + scales/zps). */
 size_t dllm_linear_weight_bytes(dllm_linear_t h);
-/* Tuning knob (benchmarks / A-B runs): selects the prefill GEMM schedule variant 0..3. */
+/* Tuning knob (benchmarks / A-B runs).  4 (default): tile policy over the 3-stage-ring kernels
+ * (256x256, 256x128, 128x128 + split-K); 5: same; 0..3: the 2-stage 256x128 schedules;
+ * 6: 2-stage kernels with 128-row tiles + split-K below 256 tiles; 16..23: decode-kernel
+ * ablation mask (measurement only: replaces loads by constants, results are garbage). */
 int dllm_linear_set_kernel_variant(dllm_linear_t h, int variant);
 int dllm_linear_destroy(dllm_linear_t h);
 

@@ -275,6 +275,48 @@ def test_linear_full_size_vs_torch_fp32(dllm, torch, orc):
     assert rel <= REL_TOL, rel
 
 
+@pytest.mark.parametrize("M", [65, 256, 512, 1024, 1500, 2048])
+def test_linear_mid_m_paths_vs_torch_fp32(dllm, torch, orc, M):
+    """Mid-M dispatch at K=N=4096: 128-row tiles with K split into 8/4/2 slices (M = 65/256/512,
+    slab partials + ordered combine) or unsplit (1024, 1500), and the 256-row tile (2048), each
+    within tolerance of the f32 product of the exported weights, for f16 and f32 outputs with
+    bias; the other schedules (variants 3, 5, 6) agree too."""
+    K = N = 4096
+    g = torch.Generator(device="cuda").manual_seed(M)
+    W = 0.02 * torch.randn(K, N, device="cuda", generator=g)
+    b = 0.1 * torch.randn(N, device="cuda", generator=g)
+    X = torch.randn(M, K, device="cuda", generator=g).half()
+    lin = dllm.QuantLinear.from_weight(W, b, 4, 128)
+    codes, scales, zps = lin.export()
+    Wh = dev(torch, orc.dequantize_weights(orc.unpack_bits(host(codes), K * N, 4).reshape(K, N), host(scales),
+                                           host(zps), 128))
+    Yr = X.float() @ Wh + b
+    for ydt in (torch.float16, torch.float32):
+        Y = lin(X, out_dtype=ydt).float()
+        rel = (torch.linalg.norm(Y - Yr) / torch.linalg.norm(Yr)).item()
+        assert rel <= REL_TOL, (M, ydt, rel)
+    for var in (3, 5, 6):   # 2-stage 256-row schedule; one k-group rings; 2-stage mid-M policy
+        lin.set_kernel_variant(var)
+        Yv = lin(X, out_dtype=torch.float32)
+        rel = (torch.linalg.norm(Yv - Yr) / torch.linalg.norm(Yr)).item()
+        assert rel <= REL_TOL, (M, var, rel)
+    lin.close()
+
+
+def test_linear_split_k_exact_integers(dllm, torch, orc):
+    """Exact-integer data through the split-K path (M=256, K=1024, N=512 -> 4 slices): every
+    partial and the combine are exact, so the result equals the f64 product bit for bit."""
+    K, N, M = 1024, 512, 256
+    rng = np.random.default_rng(21)
+    W = rng.integers(0, 16, (K, N)).astype(np.float32)
+    for g0 in range(0, K, 128):
+        W[g0, :], W[g0 + 1, :] = 0.0, 15.0
+    X = rng.integers(-2, 3, (M, K)).astype(np.float32)
+    lin = dllm.QuantLinear.from_weight(dev(torch, W), None, 4, 128)
+    Y = host(lin(dev(torch, X).half(), out_dtype=torch.float32))
+    assert np.array_equal(Y, (X.astype(np.float64) @ W.astype(np.float64)).astype(np.float32))
+
+
 def test_mixed_precision_stack(dllm, torch, orc):
     """Config 3 shape family: layers cycle bits [2, 4]; each layer within tolerance of the f32
     restatement applied to the same f16 input."""
