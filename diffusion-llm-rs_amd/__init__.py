@@ -11,23 +11,28 @@ this package is the host-side mirror of the reference's Rust operator surface:
 * ``kvquant``      -- ``prefill_kvquant_rs::kvquant`` (BitQuantizer, PrefillKVQuant, SystemConfig)
   and ``diffusion_prefill``'s compress/decompress_vector.
 * ``linear``       -- the int2/int4/int8 group-quantized linear layer (dequant + MFMA GEMM).
+* ``diffusion``    -- ``diffuse_llm``'s schedules, add_noise / p_sample (seeded device noise), the
+  phase-aware KVCacheEntry and the denoise loop (last layer fused with p_sample).
 """
 from . import _lib
 from ._lib import (CalibrationRequired, HipError, InvalidParams, QuantizationError, ShapeMismatch,
                    UnsupportedOperation)
-from . import quantization, quant, kvquant, linear, parallel
+from . import quantization, quant, kvquant, linear, parallel, diffusion
 from .quantization import (QuantizedKVCacheEntry, QuantizedTensor, compression_ratio, dequantize_tensor, kv_attention,
                            pack, quantize_tensor, unpack)
 from .quant import CalibrationData, DefaultQuantizer, QuantizationParams, QuantizationType, quant_utils
 from .kvquant import BitQuantizer, PrefillKVQuant, SystemConfig, compress_vectors, decompress_vectors
 from .linear import MixedPrecisionStack, QuantLinear
+from .diffusion import (AlphaMode, BetaSchedule, Cumprod, DenoiseLoop, DiffusionConfig, KVCacheEntry, add_noise,
+                        p_sample, randn)
 
 __all__ = [
     "quantize_tensor", "dequantize_tensor", "pack", "unpack", "compression_ratio", "QuantizedTensor",
     "QuantizedKVCacheEntry", "kv_attention", "QuantizationType", "QuantizationParams", "DefaultQuantizer", "quant_utils",
     "CalibrationData", "BitQuantizer", "PrefillKVQuant", "SystemConfig", "compress_vectors", "decompress_vectors",
     "QuantLinear", "MixedPrecisionStack", "QuantizationError", "InvalidParams", "UnsupportedOperation",
-    "ShapeMismatch", "CalibrationRequired", "HipError",
+    "ShapeMismatch", "CalibrationRequired", "HipError", "BetaSchedule", "Cumprod", "AlphaMode", "DiffusionConfig",
+    "KVCacheEntry", "DenoiseLoop", "add_noise", "p_sample", "randn",
 ]
 
 

@@ -64,6 +64,7 @@ _ERRORS = {ERR_INVALID_PARAMS: InvalidParams, ERR_UNSUPPORTED: UnsupportedOperat
            ERR_HIP: HipError, ERR_NO_DEVICE: HipError}
 
 P, S, U8, I32, U32, FL, INT = (C.c_void_p, C.c_size_t, C.c_uint8, C.c_int32, C.c_uint32, C.c_float, C.c_int)
+U64 = C.c_uint64
 
 # name -> (restype, argtypes); the authoritative list of exported entry points.
 SIGNATURES = {
@@ -96,6 +97,14 @@ SIGNATURES = {
     "dllm_linear_set_kernel_variant": (INT, [P, INT]),
     "dllm_linear_destroy": (INT, [P]),
     "dllm_kv_attention": (INT, [P, P, P, P, P, U8, S, S, S, P, P]),
+    "dllm_beta_schedule": (INT, [INT, S, FL, FL, P]),
+    "dllm_alpha_bars": (INT, [P, S, INT, P, P]),
+    "dllm_p_sample_coeffs": (INT, [P, S, INT, INT, P, S, P, P]),
+    "dllm_add_noise_coeffs": (INT, [P, S, INT, P, S, P]),
+    "dllm_randn": (INT, [U64, U64, P, S, P]),
+    "dllm_p_sample": (INT, [P, P, P, P, S, S, INT, U64, U64, P, P]),
+    "dllm_add_noise": (INT, [P, P, P, S, S, U64, U64, P, P, P]),
+    "dllm_linear_forward_psample": (INT, [P, P, S, INT, P, P, S, INT, U64, U64, P, P]),
     "dllm_quantize_tensor_host": (INT, [P, S, U8, P, P, P]),
     "dllm_dequantize_tensor_host": (INT, [P, S, FL, FL, P]),
     "dllm_default_quantize_host": (INT, [P, S, INT, FL, I32, P]),

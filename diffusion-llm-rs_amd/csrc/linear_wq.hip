@@ -17,9 +17,11 @@
 //   Per (group, column) one u32 `sz` = f16 pair {-(1024 + zp), f16(scale)}:
 //   f16(q - zp) is exact (|q - zp| < 2048), then one f16 rounding of (q - zp) * f16(scale).
 #include "common.hpp"
+#include "diffusion_rng.hpp"
 
 #include <algorithm>
 #include <map>
+#include <tuple>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -53,6 +55,34 @@ namespace dllm {
 namespace {
 
 constexpr int kBM = 256, kBN = 128, kBK = 64, kThreads = 256;
+
+// Fused p_sample epilogue (dllm_linear_forward_psample): eps = acc + bias (f32) becomes
+// x_prev = (c1 x_t + c2 eps) + std * n, n = stream element offset + m N + n (or 0).
+struct PSampleEpi {
+    const float *x_t;
+    const float *coef;    // [M / rps][3]
+    int rps;              // rows per sample
+    int add;
+    uint64_t seed, offset;
+    float *x_prev;
+};
+
+// Four consecutive outputs (m, n..n+3) of the fused epilogue; N % 4 == 0, offset % 4 == 0.
+__device__ __forceinline__ void psample4(const PSampleEpi &e, int m, int n, int N, float e0, float e1, float e2,
+                                         float e3) {
+    const size_t i = static_cast<size_t>(m) * N + n;
+    const float *c = e.coef + 3 * (m / e.rps);
+    const float c1 = c[0], c2 = c[1], sd = c[2];
+    float z[4] = {0.f, 0.f, 0.f, 0.f};
+    if (e.add) rng::normal4(e.seed, (e.offset + i) / 4, z);
+    const float4 x = *reinterpret_cast<const float4 *>(e.x_t + i);
+    float4 o;
+    o.x = (c1 * x.x + c2 * e0) + sd * z[0];
+    o.y = (c1 * x.y + c2 * e1) + sd * z[1];
+    o.z = (c1 * x.z + c2 * e2) + sd * z[2];
+    o.w = (c1 * x.w + c2 * e3) + sd * z[3];
+    *reinterpret_cast<float4 *>(e.x_prev + i) = o;
+}
 
 inline size_t canon_words(size_t K, size_t N, int bits) { return (K * N * bits + 31) / 32; }
 
@@ -172,6 +202,17 @@ __global__ void __launch_bounds__(256) cast_f32_f16_kernel(const float *__restri
     }
     for (size_t i = n4 * 4 + blockIdx.x * static_cast<size_t>(256) + threadIdx.x; i < n; i += stride)
         y[i] = __float2half_rn(x[i]);
+}
+
+// Row coefficient table: out[m] = coef[m / rps] (3 floats each).
+__global__ void __launch_bounds__(256) expand_coef_kernel(const float *__restrict__ coef, size_t M, size_t rps,
+                                                          float *__restrict__ out) {
+    for (size_t m = blockIdx.x * static_cast<size_t>(256) + threadIdx.x; m < M; m += static_cast<size_t>(gridDim.x) * 256) {
+        const float *c = coef + 3 * (m / rps);
+        out[3 * m] = c[0];
+        out[3 * m + 1] = c[1];
+        out[3 * m + 2] = c[2];
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -542,11 +583,13 @@ struct StageLayout8 {
 // 4/KG substeps kg*4/KG ..: KG = 2 puts two waves on each SIMD at the same tile count (the 128-row
 // tiles of mid-M shapes run one block per CU), their two accumulators summed through the stage
 // LDS at the end (fixed order).  SPLIT: as wq_gemm_kernel (slab partial, no bias).
-template <int BITS, typename YT, int NW = 8, int MR = kMReps, bool SPLIT = false, int KG = 1, int LAB = 0>
+template <int BITS, typename YT, int NW = 8, int MR = kMReps, bool SPLIT = false, int KG = 1, int LAB = 0,
+          int EPI = 0>
 __global__ void __launch_bounds__(NW * KG * 64, (NW * KG == 8 || MR == 8) ? 1 : 2)
 wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdev,
                 const uint32_t *__restrict__ sz, const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad,
-                int group, int nbm, int nbn, int nsplit = 1, float *__restrict__ ws = nullptr) {
+                int group, int nbm, int nbn, int nsplit = 1, float *__restrict__ ws = nullptr,
+                PSampleEpi epi = PSampleEpi{}) {
     using SL = StageLayout8<BITS, NW, MR, KG>;
     constexpr int kBMt = 32 * MR, kBNt = 32 * NW, kWT = NW * KG, kSub = 4 / KG;
     static_assert(SL::kXRounds >= 1 && 4 * MR % kWT == 0, "X staging must split evenly over the waves");
@@ -768,6 +811,20 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
     float4 bv[4];
 #pragma unroll
     for (int qd = 0; qd < 4; ++qd) bv[qd] = *reinterpret_cast<const float4 *>(bias + nb0 + 8 * qd);
+    if constexpr (EPI == 1) {
+#pragma unroll
+        for (int r = 0; r < MR; ++r) {
+            const int m = m0 + r * 32 + (lane & 31);
+            if (m >= M) continue;
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd) {
+                if (nb0 + 8 * qd >= N) continue;
+                psample4(epi, m, nb0 + 8 * qd, N, acc[r][4 * qd + 0] + bv[qd].x, acc[r][4 * qd + 1] + bv[qd].y,
+                         acc[r][4 * qd + 2] + bv[qd].z, acc[r][4 * qd + 3] + bv[qd].w);
+            }
+        }
+        return;
+    }
     const bool full = (m0 + kBMt <= M) && (n0 + kBNt <= N) && (N % 4) == 0;
     if (full) {
 #pragma unroll
@@ -953,10 +1010,10 @@ void launch_prefill(const dllm_linear *h, const __half *X, int M, YT *Y, hipStre
 }
 
 // Split-K combine: Y[m][n] = sum_s ws[s][m][n] (slice order) + bias[n]; 4 outputs per thread.
-template <typename YT>
+template <typename YT, int EPI = 0>
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float *__restrict__ ws, int nsplit, int M, int N,
                                                             int Npad, const float *__restrict__ bias,
-                                                            YT *__restrict__ Y) {
+                                                            YT *__restrict__ Y, PSampleEpi epi = PSampleEpi{}) {
     const int q = Npad / 4;
     const size_t total = static_cast<size_t>(M) * q, slab = static_cast<size_t>(M) * Npad;
     const bool vec_ok = (N % 4) == 0;
@@ -970,20 +1027,25 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float *__restr
             const float4 b = *reinterpret_cast<const float4 *>(p + s * slab);
             a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
         }
-        store_out4<YT>(Y + static_cast<size_t>(m) * N, bias, n, N, vec_ok, a.x, a.y, a.z, a.w);
+        if constexpr (EPI == 1) {
+            const float4 bv = *reinterpret_cast<const float4 *>(bias + n);
+            psample4(epi, m, n, N, a.x + bv.x, a.y + bv.y, a.z + bv.z, a.w + bv.w);
+        } else {
+            store_out4<YT>(Y + static_cast<size_t>(m) * N, bias, n, N, vec_ok, a.x, a.y, a.z, a.w);
+        }
     }
 }
 
 // Split-K slab workspace, one per (device, stream): launches on one stream run in order, so every
 // layer on that stream can share it.  It only grows; a growth waits for the stream first (queued
 // kernels may still read the old one) and is refused while the stream is being captured.
-float *splitk_workspace(hipStream_t st, size_t bytes) {
+float *splitk_workspace(hipStream_t st, size_t bytes, int slot = 0) {
     static std::mutex mu;
-    static std::map<std::pair<int, hipStream_t>, std::pair<float *, size_t>> pool;
+    static std::map<std::tuple<int, hipStream_t, int>, std::pair<float *, size_t>> pool;
     int dev = 0;
     (void)hipGetDevice(&dev);
     std::lock_guard<std::mutex> lk(mu);
-    auto &e = pool[{dev, st}];
+    auto &e = pool[{dev, st, slot}];
     if (e.second >= bytes) return e.first;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     (void)hipStreamIsCapturing(st, &cs);
@@ -1035,11 +1097,13 @@ int launch_mid(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t 
 }
 
 // 3-stage-ring GEMM with tile (32 MR) x (32 NW), K optionally split into nsplit slices.
-template <int BITS, typename YT, int NW, int MR, int KG = 1>
-int launch_ring(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t st, int nsplit) {
+template <int BITS, typename YT, int NW, int MR, int KG = 1, int EPI = 0>
+int launch_ring(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t st, int nsplit,
+                const PSampleEpi *epi = nullptr) {
     const int nbm = (M + 32 * MR - 1) / (32 * MR), nbn = static_cast<int>(h->Npad / (32 * NW));
     const unsigned nb = static_cast<unsigned>(nbm * nbn * nsplit);
-    if (h->rlab != 0 && nsplit == 1) {   // measurement only
+    const PSampleEpi ep = epi ? *epi : PSampleEpi{};
+    if (EPI == 0 && h->rlab != 0 && nsplit == 1) {   // measurement only
         if (h->rlab == 1)
             wq_gemm8_kernel<BITS, YT, NW, MR, false, KG, 1><<<nb, NW * KG * 64, 0, st>>>(
                 X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn);
@@ -1053,8 +1117,9 @@ int launch_ring(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t
         return DLLM_OK;
     }
     if (nsplit == 1) {
-        wq_gemm8_kernel<BITS, YT, NW, MR, false, KG><<<nb, NW * KG * 64, 0, st>>>(
-            X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn);
+        wq_gemm8_kernel<BITS, YT, NW, MR, false, KG, 0, EPI><<<nb, NW * KG * 64, 0, st>>>(
+            X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn, 1,
+            nullptr, ep);
         DLLM_LAUNCH_CHECK();
         return DLLM_OK;
     }
@@ -1065,27 +1130,29 @@ int launch_ring(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t
     DLLM_LAUNCH_CHECK();
     const size_t q = static_cast<size_t>(M) * (h->Npad / 4);
     const unsigned rb = static_cast<unsigned>(std::min<size_t>((q + 255) / 256, 4 * kCUs));
-    splitk_reduce_kernel<YT><<<rb, 256, 0, st>>>(ws, nsplit, M, (int)h->N, (int)h->Npad, h->bias, Y);
+    splitk_reduce_kernel<YT, EPI><<<rb, 256, 0, st>>>(ws, nsplit, M, (int)h->N, (int)h->Npad, h->bias, Y, ep);
     DLLM_LAUNCH_CHECK();
     return DLLM_OK;
 }
 
 // Tile policy (variant 4, the default): the largest tile that still gives >= 256 blocks; below
 // that, 128 x 128 tiles with K split until ~200+ blocks (slab partials + ordered combine).
-template <int BITS, typename YT>
-int launch_auto(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t st) {
+template <int BITS, typename YT, int EPI = 0>
+int launch_auto(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t st,
+                const PSampleEpi *epi = nullptr) {
     const int np = static_cast<int>(h->Npad);
     const int mb256 = (M + 255) / 256, mb128 = (M + 127) / 128;
-    if (np % 256 == 0 && mb256 * (np / 256) >= kCUs) return launch_ring<BITS, YT, 8, 8>(h, X, M, Y, st, 1);
+    if (np % 256 == 0 && mb256 * (np / 256) >= kCUs) return launch_ring<BITS, YT, 8, 8, 1, EPI>(h, X, M, Y, st, 1, epi);
     const bool kg2 = h->variant == 4;   // variant 5: the same tiles with one k-group (A/B)
     if (mb256 * (np / 128) >= kCUs)
-        return kg2 ? launch_ring<BITS, YT, 4, 8, 2>(h, X, M, Y, st, 1) : launch_ring<BITS, YT, 4, 8, 1>(h, X, M, Y, st, 1);
+        return kg2 ? launch_ring<BITS, YT, 4, 8, 2, EPI>(h, X, M, Y, st, 1, epi)
+                   : launch_ring<BITS, YT, 4, 8, 1, EPI>(h, X, M, Y, st, 1, epi);
     const int tiles = mb128 * (np / 128);
     const int nk = static_cast<int>(h->K / kBK);
     int nsplit = 1;
     while (tiles * nsplit < 200 && nsplit < 8 && nk % (2 * nsplit) == 0 && nk / (2 * nsplit) >= 4) nsplit *= 2;
-    return kg2 ? launch_ring<BITS, YT, 4, 4, 2>(h, X, M, Y, st, nsplit)
-               : launch_ring<BITS, YT, 4, 4, 1>(h, X, M, Y, st, nsplit);
+    return kg2 ? launch_ring<BITS, YT, 4, 4, 2, EPI>(h, X, M, Y, st, nsplit, epi)
+               : launch_ring<BITS, YT, 4, 4, 1, EPI>(h, X, M, Y, st, nsplit, epi);
 }
 
 template <int BITS, typename YT>
@@ -1104,6 +1171,11 @@ int launch_gemm_t(const dllm_linear *h, const __half *X, size_t M, YT *Y, hipStr
     }
     DLLM_LAUNCH_CHECK();
     return DLLM_OK;
+}
+
+template <int BITS>
+int psample_fused(dllm_linear *h, const __half *Xh, int M, const PSampleEpi &ep, hipStream_t st) {
+    return launch_auto<BITS, float, 1>(h, Xh, M, ep.x_prev, st, &ep);
 }
 
 template <int BITS>
@@ -1213,6 +1285,31 @@ int dllm_linear_create_quantized(const uint8_t *packed_codes, const float *scale
     return DLLM_OK;
 }
 
+// f16 view of X: as given, or cast from f32 through the handle's workspace.
+static int prepare_x(dllm_linear *h, const void *X, size_t M, int x_dtype, hipStream_t st, const __half **Xh) {
+    *Xh = static_cast<const __half *>(X);
+    if (x_dtype != DLLM_F32) return DLLM_OK;
+    std::lock_guard<std::mutex> lk(h->mu);
+    const size_t need = M * h->K;
+    if (h->xws_elems < need) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        (void)hipStreamIsCapturing(st, &cs);
+        if (cs != hipStreamCaptureStatusNone)
+            return fail(DLLM_ERR_INVALID_PARAMS, "f32 X workspace must be grown before stream capture");
+        DLLM_HIP_TRY(hipStreamSynchronize(st));
+        (void)hipFree(h->xws);
+        h->xws = nullptr;
+        h->xws_elems = 0;
+        DLLM_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&h->xws), need * sizeof(__half)));
+        h->xws_elems = need;
+    }
+    cast_f32_f16_kernel<<<grid_for(need / 4 + 1, 256, kCUs * 8), 256, 0, st>>>(static_cast<const float *>(X), need,
+                                                                                 h->xws);
+    DLLM_LAUNCH_CHECK();
+    *Xh = h->xws;
+    return DLLM_OK;
+}
+
 int dllm_linear_forward(dllm_linear_t h, const void *X, size_t M, int x_dtype, void *Y, int y_dtype,
                         dllm_stream_t stream) {
     if (!h) return fail(DLLM_ERR_INVALID_PARAMS, "null handle");
@@ -1224,31 +1321,58 @@ int dllm_linear_forward(dllm_linear_t h, const void *X, size_t M, int x_dtype, v
     if ((reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(Y) & 15))
         return fail(DLLM_ERR_INVALID_PARAMS, "X and Y must be 16-byte aligned");
     hipStream_t st = as_stream(stream);
-    const __half *Xh = static_cast<const __half *>(X);
-    if (x_dtype == DLLM_F32) {
-        std::lock_guard<std::mutex> lk(h->mu);
-        const size_t need = M * h->K;
-        if (h->xws_elems < need) {
-            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-            (void)hipStreamIsCapturing(st, &cs);
-            if (cs != hipStreamCaptureStatusNone)
-                return fail(DLLM_ERR_INVALID_PARAMS, "f32 X workspace must be grown before stream capture");
-            DLLM_HIP_TRY(hipStreamSynchronize(st));
-            (void)hipFree(h->xws);
-            h->xws = nullptr;
-            h->xws_elems = 0;
-            DLLM_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&h->xws), need * sizeof(__half)));
-            h->xws_elems = need;
-        }
-        cast_f32_f16_kernel<<<grid_for(need / 4 + 1, 256, kCUs * 8), 256, 0, st>>>(static_cast<const float *>(X),
-                                                                                     need, h->xws);
-        DLLM_LAUNCH_CHECK();
-        Xh = h->xws;
-    }
+    const __half *Xh = nullptr;
+    if (const int rc = prepare_x(h, X, M, x_dtype, st, &Xh)) return rc;
     switch (h->bits) {
     case 2: return launch_gemm<2>(h, Xh, M, Y, y_dtype, st);
     case 4: return launch_gemm<4>(h, Xh, M, Y, y_dtype, st);
     case 8: return launch_gemm<8>(h, Xh, M, Y, y_dtype, st);
+    default: return fail(DLLM_ERR_UNSUPPORTED, "bits");
+    }
+}
+
+int dllm_linear_forward_psample(dllm_linear_t h, const void *X, size_t M, int x_dtype, const float *x_t,
+                                const float *coef, size_t rows_per_sample, int add_noise, uint64_t seed,
+                                uint64_t offset, float *x_prev, dllm_stream_t stream) {
+    if (!h) return fail(DLLM_ERR_INVALID_PARAMS, "null handle");
+    if (x_dtype != DLLM_F32 && x_dtype != DLLM_F16) return fail(DLLM_ERR_UNSUPPORTED, "x_dtype");
+    if (M == 0) return DLLM_OK;
+    if (!X || !x_t || !coef || !x_prev || rows_per_sample == 0) return fail(DLLM_ERR_INVALID_PARAMS, "null argument");
+    if (M > (1u << 30)) return fail(DLLM_ERR_SHAPE_MISMATCH, "M too large");
+    if (h->N % 4) return fail(DLLM_ERR_UNSUPPORTED, "fused p_sample needs N % 4 == 0");
+    if (offset % 4) return fail(DLLM_ERR_INVALID_PARAMS, "offset must be a multiple of 4");
+    if ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(x_t) | reinterpret_cast<uintptr_t>(x_prev)) & 15)
+        return fail(DLLM_ERR_INVALID_PARAMS, "X, x_t and x_prev must be 16-byte aligned");
+    hipStream_t st = as_stream(stream);
+    const __half *Xh = nullptr;
+    if (const int rc = prepare_x(h, X, M, x_dtype, st, &Xh)) return rc;
+    if (M <= static_cast<size_t>(kDecodeMaxM) || (h->variant != 4 && h->variant != 5)) {
+        // Paths without the fused epilogue: f32 eps through a per-stream workspace, then p_sample
+        // (the same eps bits, hence the same result as the fused form on that path).
+        float *eps = splitk_workspace(st, M * h->N * sizeof(float), 1);
+        if (!eps) return DLLM_ERR_HIP;
+        int rc = DLLM_OK;
+        switch (h->bits) {
+        case 2: rc = launch_gemm<2>(h, Xh, M, eps, DLLM_F32, st); break;
+        case 4: rc = launch_gemm<4>(h, Xh, M, eps, DLLM_F32, st); break;
+        default: rc = launch_gemm<8>(h, Xh, M, eps, DLLM_F32, st); break;
+        }
+        if (rc) return rc;
+        // Per-row coefficients: expand the per-sample table when samples span several rows.
+        if (rows_per_sample != 1) {
+            float *rc3 = splitk_workspace(st, M * 3 * sizeof(float), 2);
+            if (!rc3) return DLLM_ERR_HIP;
+            expand_coef_kernel<<<grid_for(M, 256, kCUs), 256, 0, st>>>(coef, M, rows_per_sample, rc3);
+            DLLM_LAUNCH_CHECK();
+            coef = rc3;
+        }
+        return dllm_p_sample(x_t, eps, nullptr, coef, M, h->N, add_noise, seed, offset, x_prev, stream);
+    }
+    const PSampleEpi ep{x_t, coef, static_cast<int>(rows_per_sample), add_noise ? 1 : 0, seed, offset, x_prev};
+    switch (h->bits) {
+    case 2: return psample_fused<2>(h, Xh, (int)M, ep, st);
+    case 4: return psample_fused<4>(h, Xh, (int)M, ep, st);
+    case 8: return psample_fused<8>(h, Xh, (int)M, ep, st);
     default: return fail(DLLM_ERR_UNSUPPORTED, "bits");
     }
 }

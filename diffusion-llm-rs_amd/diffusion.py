@@ -1,0 +1,314 @@
+"""The diffusion-step ops either side of the denoiser and the denoise loop (SURVEY.md 8f rank 1-2,
+config C5), mirroring ``diffuse_llm_rs::diffuse_llm`` (diffuse-llm-rs/src/lib.rs):
+
+* ``DiffusionConfig.create_beta_schedule``  -- lib.rs:554-593 (host scalars, Rust f32 semantics)
+* ``add_noise``                             -- DiffuseLLM::add_noise, lib.rs:1100-1137
+* ``p_sample``                              -- DiffuseLLM::p_sample, lib.rs:1152-1215
+* ``KVCacheEntry``                          -- phase-aware dual-precision KV cache, lib.rs:121-313
+* ``DenoiseLoop``                           -- DiffuseLLM::sample, lib.rs:853-955, with an
+  L-layer quantized denoiser whose last layer runs p_sample in its GEMM epilogue.
+
+Reference conventions that the code gets wrong or leaves open are explicit arguments (see
+include/dllm_quant.h): ``cumprod`` (exclusive alpha-bar of add_noise/p_sample, whose t = 0
+step divides by zero, vs the inclusive p_losses scan) and ``alpha_mode`` (per-sample alpha_t vs
+the reference's full-length ``alphas`` broadcast).  Noise is the build's seeded stream
+(``randn``), not thread_rng.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from enum import IntEnum
+from typing import Callable, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check
+from .quantization import QuantizedKVCacheEntry
+
+
+class BetaSchedule(IntEnum):
+    """lib.rs:111-118."""
+    Linear = 0
+    Quadratic = 1
+    Cosine = 2
+
+
+class Cumprod(IntEnum):
+    EXCLUSIVE = 0   # add_noise / p_sample (lib.rs:1116-1119, 1162-1165)
+    INCLUSIVE = 1   # p_losses (lib.rs:627-630)
+
+
+class AlphaMode(IntEnum):
+    PER_SAMPLE = 0  # alpha[t_i] (the posterior the code intends)
+    LITERAL = 1     # full-length `alphas` row-wise (lib.rs:1191; batch == num_timesteps only)
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr() if isinstance(t, torch.Tensor) else t.ctypes.data)
+
+
+def _stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+@dataclass
+class DiffusionConfig:
+    """lib.rs:456-488 (DiffusionConfig::default) plus the phase-aware KV fields DiffuseLLM::sample
+    reads (lib.rs:880-903)."""
+    num_timesteps: int = 1000
+    hidden_size: int = 768
+    num_layers: int = 12
+    num_attention_heads: int = 12
+    vocab_size: int = 50257
+    max_sequence_length: int = 1024
+    beta_start: float = 0.0001
+    beta_end: float = 0.02
+    beta_schedule: BetaSchedule = BetaSchedule.Linear
+    use_kv_cache: bool = True
+    kv_quant_bits: int = 4
+    max_cache_size: int = 2 * 1024 * 1024 * 1024
+    use_phase_aware_quant: bool = True
+    prefill_bits: int = 8
+    decode_bits: int = 4
+    min_decode_bits: int = 2
+    progressive_precision: bool = False
+
+    def create_beta_schedule(self) -> np.ndarray:
+        """lib.rs:554-593 -> f32 [num_timesteps] (host)."""
+        out = np.zeros(self.num_timesteps, np.float32)
+        check(_lib.load().dllm_beta_schedule(int(self.beta_schedule), self.num_timesteps, float(self.beta_start),
+                                             float(self.beta_end), _ptr(out)))
+        return out
+
+    def alpha_bars(self, cumprod: Cumprod = Cumprod.EXCLUSIVE):
+        betas = self.create_beta_schedule()
+        a = np.zeros_like(betas)
+        ab = np.zeros_like(betas)
+        check(_lib.load().dllm_alpha_bars(_ptr(betas), betas.size, int(cumprod), _ptr(a), _ptr(ab)))
+        return a, ab
+
+
+def randn(n: int, seed: int, offset: int = 0, device="cuda") -> torch.Tensor:
+    """Elements offset .. offset + n - 1 of the seeded N(0, 1) stream (f32, device)."""
+    out = torch.empty(n, dtype=torch.float32, device=device)
+    check(_lib.load().dllm_randn(seed, offset, _ptr(out), n, _stream()))
+    return out
+
+
+def _timesteps(t, B):
+    t = np.asarray([t] * B if np.isscalar(t) else t, dtype=np.uint64)
+    if t.size != B:
+        raise _lib.ShapeMismatch("Timesteps must match batch size")   # lib.rs:624
+    return t
+
+
+def p_sample_coeffs(config: DiffusionConfig, t, B: int, cumprod=Cumprod.EXCLUSIVE, alpha_mode=AlphaMode.PER_SAMPLE):
+    """Per-sample {c1, c2, std} (host f32 [B, 3]) and the reference's noise flag (t[0] > 0)."""
+    betas = config.create_beta_schedule()
+    tt = _timesteps(t, B)
+    coef = np.zeros((B, 3), np.float32)
+    flag = C.c_int(0)
+    check(_lib.load().dllm_p_sample_coeffs(_ptr(betas), betas.size, int(cumprod), int(alpha_mode), _ptr(tt), B,
+                                           _ptr(coef), C.byref(flag)))
+    return coef, bool(flag.value)
+
+
+def add_noise_coeffs(config: DiffusionConfig, t, B: int, cumprod=Cumprod.EXCLUSIVE):
+    betas = config.create_beta_schedule()
+    tt = _timesteps(t, B)
+    coef = np.zeros((B, 2), np.float32)
+    check(_lib.load().dllm_add_noise_coeffs(_ptr(betas), betas.size, int(cumprod), _ptr(tt), B, _ptr(coef)))
+    return coef
+
+
+def _dev32(x):
+    return x.to(device="cuda", dtype=torch.float32).contiguous()
+
+
+def add_noise(config: DiffusionConfig, x_start: torch.Tensor, t, noise: Optional[torch.Tensor] = None, seed: int = 0,
+              offset: int = 0, cumprod: Cumprod = Cumprod.EXCLUSIVE):
+    """DiffuseLLM::add_noise (lib.rs:1100-1137): (noisy, noise) for x_start [B, D]."""
+    x0 = _dev32(x_start)
+    B, D = x0.shape
+    coef = torch.from_numpy(add_noise_coeffs(config, t, B, cumprod)).to(x0.device)
+    noisy = torch.empty_like(x0)
+    if noise is None:
+        nz = torch.empty_like(x0)
+        check(_lib.load().dllm_add_noise(_ptr(x0), None, _ptr(coef), B, D, seed, offset, _ptr(noisy), _ptr(nz),
+                                         _stream()))
+    else:
+        nz = _dev32(noise)
+        if nz.shape != x0.shape:
+            raise _lib.ShapeMismatch("Noise shape must match input shape")   # lib.rs:623
+        check(_lib.load().dllm_add_noise(_ptr(x0), _ptr(nz), _ptr(coef), B, D, 0, 0, _ptr(noisy), None, _stream()))
+    return noisy, nz
+
+
+def p_sample(config: DiffusionConfig, x_t: torch.Tensor, t, noise_pred: torch.Tensor, seed: int = 0,
+             offset: int = 0, noise: Optional[torch.Tensor] = None, cumprod: Cumprod = Cumprod.EXCLUSIVE,
+             alpha_mode: AlphaMode = AlphaMode.PER_SAMPLE, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """DiffuseLLM::p_sample (lib.rs:1152-1215) for x_t, noise_pred [B, D]."""
+    x = _dev32(x_t)
+    eps = _dev32(noise_pred)
+    B, D = x.shape
+    coef_np, flag = p_sample_coeffs(config, t, B, cumprod, alpha_mode)
+    coef = torch.from_numpy(coef_np).to(x.device)
+    out = torch.empty_like(x) if out is None else out
+    nz = None if noise is None else _dev32(noise)
+    check(_lib.load().dllm_p_sample(_ptr(x), _ptr(eps), None if nz is None else _ptr(nz), _ptr(coef), B, D, int(flag),
+                                    seed, offset, _ptr(out), _stream()))
+    return out
+
+
+class KVCacheEntry:
+    """Phase-aware dual-precision KV cache (lib.rs:121-313): f32 K/V [layers, seq, hidden] on
+    the device plus a prefill-width and a decode-width QuantizedKVCacheEntry (per-tensor a1
+    codes, packed).  ``update`` re-quantizes both copies on the GPU (the reference's up-to-4
+    quantize_tensor calls per timestep); ``get_keys``/``get_values`` dequantize the copy of the
+    current phase."""
+
+    def __init__(self, keys: torch.Tensor, values: torch.Tensor, prefill_bits: int, decode_bits: int):
+        self.keys, self.values = keys, values
+        self.prefill_quant_bits, self.decode_quant_bits = prefill_bits, decode_bits
+        self.prefill_quantized = QuantizedKVCacheEntry.new(keys, values, prefill_bits) if prefill_bits > 0 else None
+        self.decode_quantized = QuantizedKVCacheEntry.new(keys, values, decode_bits) if decode_bits > 0 else None
+        self.is_prefill_phase = True
+        self.seq_len = int(keys.shape[1])
+
+    @classmethod
+    def new(cls, keys, values, prefill_bits, decode_bits):
+        return cls(keys, values, prefill_bits, decode_bits)
+
+    def _current(self):
+        return self.prefill_quantized if self.is_prefill_phase else self.decode_quantized
+
+    def get_keys(self) -> torch.Tensor:
+        q = self._current()
+        return self.keys.clone() if q is None else q.dequantize_keys()
+
+    def get_values(self) -> torch.Tensor:
+        q = self._current()
+        return self.values.clone() if q is None else q.dequantize_values()
+
+    def get_current_quant_bits(self) -> int:
+        return self.prefill_quant_bits if self.is_prefill_phase else self.decode_quant_bits
+
+    def set_phase(self, is_prefill: bool):
+        self.transition_phase(is_prefill)
+
+    def transition_phase(self, is_prefill: bool):
+        """lib.rs:221-239."""
+        if self.is_prefill_phase == is_prefill:
+            return
+        self.is_prefill_phase = is_prefill
+        if not is_prefill and self.decode_quant_bits > 0 and self.decode_quantized is None:
+            self.decode_quantized = QuantizedKVCacheEntry.new(self.keys, self.values, self.decode_quant_bits)
+
+    def update(self, new_keys: torch.Tensor, new_values: torch.Tensor):
+        """lib.rs:241-276 (the missing QuantizedKVCacheEntry::update is a re-quantization)."""
+        self.keys, self.values = new_keys, new_values
+        self.seq_len = int(new_keys.shape[1])
+        if self.prefill_quant_bits > 0:
+            self.prefill_quantized = QuantizedKVCacheEntry.new(new_keys, new_values, self.prefill_quant_bits)
+        if self.decode_quant_bits > 0:
+            self.decode_quantized = QuantizedKVCacheEntry.new(new_keys, new_values, self.decode_quant_bits)
+
+    def memory_usage(self) -> int:
+        """lib.rs:279-302: packed bytes of the quantized copies, else f32 bytes."""
+        total = sum(q.memory_usage() for q in (self.prefill_quantized, self.decode_quantized) if q is not None)
+        return total if total else (self.keys.numel() + self.values.numel()) * 4
+
+    def __len__(self):
+        return self.seq_len
+
+    def is_empty(self) -> bool:
+        return self.seq_len == 0
+
+
+def progressive_bits(config: DiffusionConfig, num_steps: int, t: int) -> int:
+    """lib.rs:890-897: decode bits interpolated towards min_decode_bits over the decode half (f32
+    arithmetic, `as u8` truncation)."""
+    progress = np.float32(num_steps - t) / np.float32(num_steps // 2)
+    v = np.float32(np.float32(config.decode_bits) * (np.float32(1.0) - progress)) + \
+        np.float32(np.float32(config.min_decode_bits) * progress)
+    return int(min(max(np.float32(v), 0), 255)) if np.isfinite(v) else 0
+
+
+class DenoiseLoop:
+    """DiffuseLLM::sample (lib.rs:853-955) over an L-layer quantized denoiser (config C5).
+
+    Per timestep t = num_steps-1 .. 0: the KV phase switch and re-quantization (KVCacheEntry),
+    the denoiser (layers 0..L-2 chained in f16, f32 x in / f32 eps out), and p_sample.  With local
+    QuantLinear layers the last layer runs p_sample inside its GEMM epilogue
+    (dllm_linear_forward_psample); a layer callable without that entry point (e.g. a
+    tensor-parallel pair whose output is all-reduced) is followed by the p_sample kernel.
+    x is [M, d] f32 for one sample of M = seq tokens (the reference's [batch, hidden*seq] row
+    laid out token-major); the noise of step i is stream elements [i M d, (i+1) M d)."""
+
+    def __init__(self, layers: Sequence, config: DiffusionConfig, cumprod: Cumprod = Cumprod.INCLUSIVE,
+                 alpha_mode: AlphaMode = AlphaMode.PER_SAMPLE, seed: int = 0,
+                 kv_cache: Optional[KVCacheEntry] = None):
+        self.layers = list(layers)
+        self.config = config
+        self.cumprod, self.alpha_mode, self.seed = cumprod, alpha_mode, seed
+        self.kv_cache = kv_cache
+        betas = config.create_beta_schedule()
+        self._betas = betas
+        self._coef_cache = {}
+
+    def _coef(self, t: int) -> tuple[torch.Tensor, bool]:
+        if t not in self._coef_cache:
+            coef = np.zeros((1, 3), np.float32)
+            flag = C.c_int(0)
+            tt = np.asarray([t], np.uint64)
+            check(_lib.load().dllm_p_sample_coeffs(_ptr(self._betas), self._betas.size, int(self.cumprod),
+                                                   int(self.alpha_mode), _ptr(tt), 1, _ptr(coef), C.byref(flag)))
+            self._coef_cache[t] = (torch.from_numpy(coef).cuda(), bool(flag.value))
+        return self._coef_cache[t]
+
+    def step(self, x: torch.Tensor, t: int, step_index: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        M, d = x.shape
+        coef, flag = self._coef(t)
+        offset = step_index * M * d
+        h = x
+        for layer in self.layers[:-1]:
+            h = layer(h, out_dtype=torch.float16)
+        last = self.layers[-1]
+        out = torch.empty_like(x) if out is None else out
+        if hasattr(last, "forward_psample"):
+            last.forward_psample(h, x, coef, M, flag, self.seed, offset, out)
+        else:
+            eps = last(h, out_dtype=torch.float32)
+            check(_lib.load().dllm_p_sample(_ptr(x), _ptr(eps), None, _ptr(coef), 1, M * d, int(flag), self.seed,
+                                            offset, _ptr(out), _stream()))
+        return out
+
+    def kv_step(self, t: int, num_steps: int):
+        """lib.rs:880-916: phase switch, progressive decode bits, update (re-quantize), dequant."""
+        c = self.kv_cache
+        if c is None:
+            return None
+        is_prefill = t > num_steps // 2
+        c.set_phase(is_prefill)
+        if self.config.progressive_precision and not is_prefill:
+            tb = progressive_bits(self.config, num_steps, t)
+            if tb != c.decode_quant_bits:
+                c.decode_quant_bits = tb
+                c.decode_quantized = None
+        keys, values = c.keys, c.values          # SimpleDiffusionModel::update_kv_cache (:826-835)
+        k, v = c.get_keys(), c.get_values()      # what forward_with_cache receives (:910-915)
+        c.update(keys, values)
+        return k, v
+
+    def sample(self, x: torch.Tensor, num_steps: Optional[int] = None) -> torch.Tensor:
+        num_steps = num_steps or self.config.num_timesteps
+        x = x.to(device="cuda", dtype=torch.float32).contiguous()
+        buf = torch.empty_like(x)
+        for i, t in enumerate(range(num_steps - 1, -1, -1)):
+            self.kv_step(t, num_steps)
+            buf = self.step(x, t, i, out=buf)
+            x, buf = buf, x
+        return x

@@ -5,6 +5,8 @@ from __future__ import annotations
 
 import ctypes as C
 
+from typing import Optional
+
 import torch
 
 from . import _lib
@@ -56,6 +58,26 @@ class QuantLinear:
         return out
 
     __call__ = forward
+
+    def forward_psample(self, x: torch.Tensor, x_t: torch.Tensor, coef: torch.Tensor, rows_per_sample: int,
+                        add_noise: bool, seed: int, offset: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Output layer of the denoiser fused with p_sample (diffuse-llm-rs/src/lib.rs:1188-1212):
+        eps = x . W^ + b (f32) and x_prev = (c1 x_t + c2 eps) + std * noise in the GEMM epilogue.
+        x [M, K] f16/f32, x_t / out f32 [M, N], coef f32 [M / rows_per_sample, 3] (device)."""
+        if x.dim() != 2 or x.shape[1] != self.K:
+            raise _lib.ShapeMismatch(f"x must be [M, {self.K}], got {tuple(x.shape)}")
+        x = _dev(x) if (not x.is_cuda or not x.is_contiguous()) else x
+        if x.dtype not in (torch.float16, torch.float32):
+            x = x.to(torch.float16)
+        M = x.shape[0]
+        if tuple(x_t.shape) != (M, self.N) or x_t.dtype != torch.float32:
+            raise _lib.ShapeMismatch(f"x_t must be f32 [{M}, {self.N}]")
+        out = torch.empty_like(x_t) if out is None else out
+        xdt = _lib.F16 if x.dtype == torch.float16 else _lib.F32
+        check(_lib.load().dllm_linear_forward_psample(self._h, _ptr(x), M, xdt, _ptr(x_t), _ptr(coef),
+                                                      int(rows_per_sample), int(bool(add_noise)), int(seed),
+                                                      int(offset), _ptr(out), _stream()))
+        return out
 
     def export(self):
         """-> (packed codes of the [K][N] code matrix, scales [G][N] f32, zero points [G][N] u8)."""

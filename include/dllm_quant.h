@@ -183,6 +183,56 @@ int dllm_kv_attention(const void *Q, const uint8_t *Kq, const float *k_params, c
                       const float *v_params, uint8_t bits, size_t S, size_t H, size_t D, void *O,
                       dllm_stream_t stream);
 
+/* ---- 8f rank 1: diffusion-step ops either side of the denoiser --------------------------------
+ * DiffuseLLM's schedule and sampling step (diffuse-llm-rs/src/lib.rs).  Host functions compute the
+ * per-timestep / per-sample scalars with Rust f32 semantics (host arrays); the elementwise steps
+ * run on the GPU.  Reference conventions exposed as flags ("pin the chosen form"):
+ *   cumprod   DLLM_ABAR_EXCLUSIVE: alpha_bar[0] = 1, alpha_bar[i] = alpha_bar[i-1] alpha[i-1]
+ *             (add_noise :1116-1119 and p_sample :1162-1165; gives 1 - alpha_bar = 0 at t = 0, so the
+ *             reference's last p_sample step divides by zero); DLLM_ABAR_INCLUSIVE: the p_losses
+ *             scan alpha_bar[i] = prod_{j<=i} alpha[j] (:627-630).
+ *   alpha     DLLM_ALPHA_PER_SAMPLE: mean_coeff2 uses alpha[t_i] (the intended posterior);
+ *             DLLM_ALPHA_LITERAL: the reference's full-length `alphas` row-wise (:1191), which is
+ *             an elementwise op only when batch == num_timesteps (otherwise ndarray panics).
+ * Noise: the reference draws rand::thread_rng normals (unseeded); the build uses a seeded
+ * counter-based stream: element e of (seed) = Philox4x32-10(key seed, counter e/4) + a Box-Muller
+ * of correctly rounded + - * / sqrt only (bit-reproducible on any IEEE host; see
+ * csrc/diffusion_rng.hpp).  Stream offsets must be multiples of 4. */
+enum dllm_beta_kind { DLLM_BETA_LINEAR = 0, DLLM_BETA_QUADRATIC = 1, DLLM_BETA_COSINE = 2 };
+enum dllm_cumprod { DLLM_ABAR_EXCLUSIVE = 0, DLLM_ABAR_INCLUSIVE = 1 };
+enum dllm_alpha_mode { DLLM_ALPHA_PER_SAMPLE = 0, DLLM_ALPHA_LITERAL = 1 };
+/* DiffusionConfig::create_beta_schedule (lib.rs:554-593); host betas[T]. */
+int dllm_beta_schedule(int kind, size_t T, float beta_start, float beta_end, float *betas);
+/* alphas = 1 - betas and the alpha_bar table of the given cumprod convention (host arrays). */
+int dllm_alpha_bars(const float *betas, size_t T, int cumprod, float *alphas, float *alpha_bars);
+/* p_sample scalars (lib.rs:1167-1195) for timesteps t[B] (clamped to T-1 as :1175):
+ * coef[B][3] = {c1 = sqrt(abar_prev) beta / (1 - abar), c2 = sqrt(alpha) (1 - abar_prev) / (1 - abar),
+ * std = sqrt((1 - abar_prev) / (1 - abar) beta)}; *add_noise = (t[0] > 0) (:1198). Host arrays. */
+int dllm_p_sample_coeffs(const float *betas, size_t T, int cumprod, int alpha_mode, const size_t *t, size_t B,
+                         float *coef, int *add_noise);
+/* add_noise scalars (lib.rs:1121-1133): coef[B][2] = {sqrt(abar_t), sqrt(1 - abar_t)}. Host arrays. */
+int dllm_add_noise_coeffs(const float *betas, size_t T, int cumprod, const size_t *t, size_t B, float *coef);
+/* out[i] = element offset + i of the seeded N(0,1) stream (device). */
+int dllm_randn(uint64_t seed, uint64_t offset, float *out, size_t n, dllm_stream_t stream);
+/* p_sample elementwise step (lib.rs:1197-1212) on B rows of D (device f32; coef device [B][3]):
+ * x_prev = (c1 x_t + c2 eps) + std * n, n = noise[i] if noise != NULL, else stream element
+ * offset + i of `seed`; n = 0 when add_noise == 0.  x_t, eps, x_prev 16-byte aligned. */
+int dllm_p_sample(const float *x_t, const float *eps, const float *noise, const float *coef, size_t B, size_t D,
+                  int add_noise, uint64_t seed, uint64_t offset, float *x_prev, dllm_stream_t stream);
+/* add_noise forward step (lib.rs:1130-1135): noisy = x0 sqrt(abar) + n sqrt(1 - abar) on B rows
+ * of D; n = noise (device) or the stream (noise == NULL; then written to noise_out if non-NULL,
+ * the reference's returned noise). */
+int dllm_add_noise(const float *x0, const float *noise, const float *coef, size_t B, size_t D, uint64_t seed,
+                   uint64_t offset, float *noisy, float *noise_out, dllm_stream_t stream);
+/* Denoiser output layer fused with p_sample: eps = X . W^ + b (f32, as dllm_linear_forward with
+ * y_dtype DLLM_F32) feeds x_prev = (c1 x_t + c2 eps) + std * n in the GEMM epilogue, with x_t and
+ * x_prev f32 [M][N] (device, may alias), coef device [M / rows_per_sample][3] (row m uses
+ * sample m / rows_per_sample) and n = stream element offset + m N + n.  Bit-identical to
+ * dllm_linear_forward(..., DLLM_F32) followed by dllm_p_sample.  N % 4 == 0. */
+int dllm_linear_forward_psample(dllm_linear_t h, const void *X, size_t M, int x_dtype, const float *x_t,
+                                const float *coef, size_t rows_per_sample, int add_noise, uint64_t seed,
+                                uint64_t offset, float *x_prev, dllm_stream_t stream);
+
 /* ---- host-slice variants (synchronous; stage through device memory; not graph-capturable) ----
  * The literal shapes of the reference's Rust signatures, for callers holding host slices. */
 /* quantize_tensor(&[f32], u8) -> (Vec<u8>, f32, f32): codes one per byte (quantization.rs:38-68). */

@@ -97,6 +97,28 @@ void orc_linear_forward(const float *X, size_t M, size_t K, const float *W, size
 void orc_attention(const float *Q, const float *K, const float *V, size_t S, size_t H, size_t D, float *O,
                    size_t q_rows, int nthreads);
 
+/* ---- 8f rank 1: diffusion-step elementwise ops (dllm_oracle_diffusion.c) ---------------- */
+enum { ORC_BETA_LINEAR = 0, ORC_BETA_QUADRATIC = 1, ORC_BETA_COSINE = 2 };
+/* DiffusionConfig::create_beta_schedule, diffuse-llm-rs/src/lib.rs:554-593 (T = 0: nothing). */
+int orc_beta_schedule(int kind, size_t T, float beta_start, float beta_end, float *betas);
+/* alphas = 1 - betas; alpha_bars: inclusive = p_losses scan (lib.rs:627-630), exclusive =
+ * add_noise / p_sample loop (lib.rs:1116-1119, 1162-1165). */
+int orc_alpha_bars(const float *betas, size_t T, int inclusive, float *alphas, float *alpha_bars);
+/* p_sample per-sample scalars (lib.rs:1167-1195), coef[B][3] = {c1, c2, std}; literal_alphas = 1
+ * takes the reference's full-length `alphas` row-wise (valid only when B == T). */
+int orc_p_sample_coeffs(const float *betas, size_t T, int inclusive, int literal_alphas, const size_t *t, size_t B,
+                        float *coef);
+/* add_noise per-sample scalars (lib.rs:1121-1133), coef[B][2] = {sqrt(abar_t), sqrt(1 - abar_t)}. */
+int orc_add_noise_coeffs(const float *betas, size_t T, int inclusive, const size_t *t, size_t B, float *coef);
+/* Build-defined seeded N(0,1) stream (Philox4x32-10 + exact-op Box-Muller), elements
+ * offset .. offset + n - 1. */
+void orc_randn(uint64_t seed, uint64_t offset, size_t n, float *out);
+/* x_prev = (c1 x_t + c2 eps) + std * (add_noise ? noise : 0), rows of D (lib.rs:1188-1212). */
+void orc_p_sample(const float *x_t, const float *eps, const float *noise, const float *coef, size_t B, size_t D,
+                  int add_noise, float *x_prev);
+/* noisy = x0 sqrt(abar) + noise sqrt(1 - abar), rows of D (lib.rs:1130-1135). */
+void orc_add_noise(const float *x0, const float *noise, const float *coef, size_t B, size_t D, float *noisy);
+
 #ifdef __cplusplus
 }
 #endif

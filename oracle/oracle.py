@@ -19,8 +19,9 @@ _lib = None
 
 
 def build(force: bool = False) -> Path:
-    src = HERE / "dllm_oracle.c"
-    if force or not LIB_PATH.exists() or LIB_PATH.stat().st_mtime < src.stat().st_mtime:
+    srcs = [HERE / "dllm_oracle.c", HERE / "dllm_oracle_diffusion.c", HERE / "dllm_oracle.h"]
+    newest = max(p.stat().st_mtime for p in srcs)
+    if force or not LIB_PATH.exists() or LIB_PATH.stat().st_mtime < newest:
         subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
     return LIB_PATH
 
@@ -49,6 +50,13 @@ def lib():
             "orc_dequantize_weights": (None, [P, P, P, S, S, S, P]),
             "orc_linear_forward": (None, [P, S, S, P, S, P, P, C.c_int]),
             "orc_attention": (None, [P, P, P, S, S, S, P, S, C.c_int]),
+            "orc_beta_schedule": (C.c_int, [C.c_int, S, F, F, P]),
+            "orc_alpha_bars": (C.c_int, [P, S, C.c_int, P, P]),
+            "orc_p_sample_coeffs": (C.c_int, [P, S, C.c_int, C.c_int, P, S, P]),
+            "orc_add_noise_coeffs": (C.c_int, [P, S, C.c_int, P, S, P]),
+            "orc_randn": (None, [C.c_uint64, C.c_uint64, S, P]),
+            "orc_p_sample": (None, [P, P, P, P, S, S, C.c_int, P]),
+            "orc_add_noise": (None, [P, P, P, S, S, P]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -192,3 +200,64 @@ def attention(Q, K, V, q_rows=None, nthreads=None):
     nthreads = nthreads or (os.cpu_count() or 1)
     lib().orc_attention(_p(Q), _p(K), _p(V), S, H, D, _p(O), q_rows, nthreads)
     return O
+
+
+# ---- 8f rank 1: diffusion-step ops -------------------------------------------------------------
+BETA_LINEAR, BETA_QUADRATIC, BETA_COSINE = 0, 1, 2
+
+
+def beta_schedule(kind, T, beta_start=0.0001, beta_end=0.02):
+    out = np.zeros(T, np.float32)
+    _check(lib().orc_beta_schedule(kind, T, beta_start, beta_end, _p(out)))
+    return out
+
+
+def alpha_bars(betas, inclusive):
+    betas = np.ascontiguousarray(betas, np.float32)
+    a = np.zeros(betas.size, np.float32)
+    ab = np.zeros(betas.size, np.float32)
+    _check(lib().orc_alpha_bars(_p(betas), betas.size, int(inclusive), _p(a), _p(ab)))
+    return a, ab
+
+
+def p_sample_coeffs(betas, t, inclusive=False, literal_alphas=False):
+    betas = np.ascontiguousarray(betas, np.float32)
+    t = np.ascontiguousarray(t, np.uint64)
+    coef = np.zeros((t.size, 3), np.float32)
+    _check(lib().orc_p_sample_coeffs(_p(betas), betas.size, int(inclusive), int(literal_alphas), _p(t), t.size,
+                                     _p(coef)))
+    return coef
+
+
+def add_noise_coeffs(betas, t, inclusive=False):
+    betas = np.ascontiguousarray(betas, np.float32)
+    t = np.ascontiguousarray(t, np.uint64)
+    coef = np.zeros((t.size, 2), np.float32)
+    _check(lib().orc_add_noise_coeffs(_p(betas), betas.size, int(inclusive), _p(t), t.size, _p(coef)))
+    return coef
+
+
+def randn(seed, offset, n):
+    out = np.zeros(n, np.float32)
+    lib().orc_randn(seed, offset, n, _p(out))
+    return out
+
+
+def p_sample(x_t, eps, noise, coef, add_noise=True):
+    x_t = np.ascontiguousarray(x_t, np.float32)
+    B, D = x_t.shape
+    eps = np.ascontiguousarray(eps, np.float32)
+    noise = np.zeros_like(x_t) if noise is None else np.ascontiguousarray(noise, np.float32)
+    out = np.zeros_like(x_t)
+    lib().orc_p_sample(_p(x_t), _p(eps), _p(noise), _p(np.ascontiguousarray(coef, np.float32)), B, D,
+                       int(add_noise), _p(out))
+    return out
+
+
+def add_noise(x0, noise, coef):
+    x0 = np.ascontiguousarray(x0, np.float32)
+    B, D = x0.shape
+    out = np.zeros_like(x0)
+    lib().orc_add_noise(_p(x0), _p(np.ascontiguousarray(noise, np.float32)),
+                        _p(np.ascontiguousarray(coef, np.float32)), B, D, _p(out))
+    return out

@@ -264,3 +264,148 @@ def linear_forward(X: np.ndarray, W: np.ndarray, bias=None) -> np.ndarray:
     if bias is not None:
         Y = Y + np.asarray(bias, np.float64)[None, :]
     return Y.astype(F32)
+
+
+# ---- 8f rank 1: diffusion-step ops (independent numpy restatement of dllm_oracle_diffusion.c) --
+# Every intermediate is forced to float32 so each step is one correctly rounded binary32 op.
+
+def beta_schedule(kind: int, T: int, beta_start=0.0001, beta_end=0.02) -> np.ndarray:
+    """DiffusionConfig::create_beta_schedule (diffuse-llm-rs/src/lib.rs:554-593).  Cosine uses
+    cos in f64 rounded to f32 (a correctly rounded cosf; glibc's cosf may differ by 1 ulp)."""
+    bs, be = F32(beta_start), F32(beta_end)
+    t = np.arange(T, dtype=F32)
+    with np.errstate(all="ignore"):
+        if kind == 0:
+            return (bs + ((be - bs) * t).astype(F32) / F32(T - 1)).astype(F32)
+        if kind == 1:
+            tn = (t / F32(T - 1)).astype(F32)
+            return (bs + (((be - bs) * tn).astype(F32) * tn).astype(F32)).astype(F32)
+        s, pi = F32(0.008), F32(np.pi)
+        tn = (t / F32(T)).astype(F32)
+        arg = (((((tn + s).astype(F32) / (F32(1.0) + s)).astype(F32) * pi).astype(F32)) / F32(2.0)).astype(F32)
+        ft = np.cos(arg.astype(np.float64)).astype(F32)
+        ft = (ft * ft).astype(F32)
+        a0 = (((s / (F32(1.0) + s)).astype(F32) * pi).astype(F32) / F32(2.0)).astype(F32)
+        f0 = F32(np.cos(np.float64(a0)))
+        f0 = F32(f0 * f0)
+        return np.fmin((F32(1.0) - (ft / f0).astype(F32)).astype(F32), F32(0.999)).astype(F32)
+
+
+def alpha_bars(betas: np.ndarray, inclusive: bool):
+    a = (F32(1.0) - np.asarray(betas, F32)).astype(F32)
+    ab = np.empty_like(a)
+    state = F32(1.0)
+    for i in range(a.size):
+        if inclusive:
+            state = F32(state * a[i])
+            ab[i] = state
+        else:
+            ab[i] = F32(1.0) if i == 0 else F32(ab[i - 1] * a[i - 1])
+    return a, ab
+
+
+def p_sample_coeffs(betas, t, inclusive=False, literal_alphas=False) -> np.ndarray:
+    a, ab = alpha_bars(betas, inclusive)
+    T = a.size
+    out = np.zeros((len(t), 3), F32)
+    with np.errstate(all="ignore"):
+        for i, ti in enumerate(t):
+            ti = min(int(ti), T - 1)
+            abar_t, beta_t = ab[ti], F32(betas[ti])
+            alpha = a[i] if literal_alphas else a[ti]
+            prev = ab[ti - 1] if ti > 0 else F32(1.0)
+            den = F32(F32(1.0) - abar_t)
+            out[i, 0] = F32(F32(np.sqrt(prev) * beta_t) / den)
+            out[i, 1] = F32(F32(np.sqrt(alpha) * F32(F32(1.0) - prev)) / den)
+            out[i, 2] = np.sqrt(F32(F32(F32(F32(1.0) - prev) / den) * beta_t))
+    return out
+
+
+def add_noise_coeffs(betas, t, inclusive=False) -> np.ndarray:
+    _, ab = alpha_bars(betas, inclusive)
+    T = ab.size
+    out = np.zeros((len(t), 2), F32)
+    for i, ti in enumerate(t):
+        ti = min(int(ti), T - 1)
+        out[i] = np.sqrt(ab[ti]), np.sqrt(F32(F32(1.0) - ab[ti]))
+    return out
+
+
+def _philox(ctr_lo, ctr_hi, seed):
+    M0, M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+    W0, W1 = np.uint32(0x9E3779B9), np.uint32(0xBB67AE85)
+    c0 = ctr_lo.astype(np.uint32)
+    c1 = ctr_hi.astype(np.uint32)
+    c2 = np.zeros_like(c0)
+    c3 = np.zeros_like(c0)
+    k0, k1 = np.uint32(seed & 0xFFFFFFFF), np.uint32(seed >> 32)
+    for _ in range(10):
+        p0 = M0 * c0.astype(np.uint64)
+        p1 = M1 * c2.astype(np.uint64)
+        hi0, lo0 = (p0 >> np.uint64(32)).astype(np.uint32), p0.astype(np.uint32)
+        hi1, lo1 = (p1 >> np.uint64(32)).astype(np.uint32), p1.astype(np.uint32)
+        c0, c1, c2, c3 = hi1 ^ c1 ^ k0, lo1, hi0 ^ c3 ^ k1, lo0
+        k0 = np.uint32((int(k0) + int(W0)) & 0xFFFFFFFF)
+        k1 = np.uint32((int(k1) + int(W1)) & 0xFFFFFFFF)
+    return c0, c1, c2, c3
+
+
+def _ln01(u):
+    bits = u.view(np.uint32)
+    e = ((bits >> np.uint32(23)) & np.uint32(0xFF)).astype(np.int32) - 127
+    m = ((bits & np.uint32(0x007FFFFF)) | np.uint32(0x3F800000)).view(F32)
+    big = m > F32(float.fromhex("0x1.6a09e6p+0"))
+    m = np.where(big, (m * F32(0.5)).astype(F32), m)
+    e = e + big.astype(np.int32)
+    s = ((m - F32(1.0)).astype(F32) / (m + F32(1.0)).astype(F32)).astype(F32)
+    s2 = (s * s).astype(F32)
+    p = np.full_like(s, F32(float.fromhex("0x1.3b13b2p-4")))
+    for c in ("0x1.745d18p-4", "0x1.c71c72p-4", "0x1.24924ap-3", "0x1.99999ap-3", "0x1.555556p-2"):
+        p = (F32(float.fromhex(c)) + (s2 * p).astype(F32)).astype(F32)
+    p = (F32(1.0) + (s2 * p).astype(F32)).astype(F32)
+    lnm = ((F32(2.0) * s).astype(F32) * p).astype(F32)
+    return ((e.astype(F32) * F32(float.fromhex("0x1.62e430p-1"))).astype(F32) + lnm).astype(F32)
+
+
+def _box_muller(ra, rb):
+    u1 = (((ra >> np.uint32(8)) + np.uint32(1)).astype(F32) * F32(2.0 ** -24)).astype(F32)
+    u2 = ((rb >> np.uint32(8)).astype(F32) * F32(2.0 ** -24)).astype(F32)
+    rad = np.sqrt((F32(-2.0) * _ln01(u1)).astype(F32)).astype(F32)
+    v = (u2 * F32(4.0)).astype(F32)
+    q = v.astype(np.int32)
+    phi = ((v - q.astype(F32)).astype(F32) * F32(float.fromhex("0x1.921fb6p+0"))).astype(F32)
+    x2 = (phi * phi).astype(F32)
+    sp = (F32(1.0) - (x2 * F32(float.fromhex("0x1.a41a42p-8"))).astype(F32)).astype(F32)
+    for c in ("0x1.29e412p-7", "0x1.c71c72p-7", "0x1.861862p-6", "0x1.99999ap-5", "0x1.555556p-3"):
+        sp = (F32(1.0) - ((x2 * F32(float.fromhex(c))).astype(F32) * sp).astype(F32)).astype(F32)
+    sn = (phi * sp).astype(F32)
+    cp = (F32(1.0) - (x2 * F32(float.fromhex("0x1.f07c20p-8"))).astype(F32)).astype(F32)
+    for c in ("0x1.6c16c2p-7", "0x1.24924ap-6", "0x1.111112p-5", "0x1.555556p-4", "0x1.0p-1"):
+        cp = (F32(1.0) - ((x2 * F32(float.fromhex(c))).astype(F32) * cp).astype(F32)).astype(F32)
+    c = np.select([q == 0, q == 1, q == 2], [cp, -sn, -cp], sn).astype(F32)
+    s = np.select([q == 0, q == 1, q == 2], [sn, cp, -sn], -cp).astype(F32)
+    return (rad * c).astype(F32), (rad * s).astype(F32)
+
+
+def randn(seed: int, offset: int, n: int) -> np.ndarray:
+    e = np.arange(offset, offset + n, dtype=np.uint64)
+    blk = e // np.uint64(4)
+    c0, c1, c2, c3 = _philox(blk & np.uint64(0xFFFFFFFF), blk >> np.uint64(32), seed)
+    z0, z1 = _box_muller(c0, c1)
+    z2, z3 = _box_muller(c2, c3)
+    lane = (e % np.uint64(4)).astype(np.int64)
+    return np.choose(lane, [z0, z1, z2, z3]).astype(F32)
+
+
+def p_sample(x_t, eps, noise, coef, add_noise=True) -> np.ndarray:
+    coef = np.asarray(coef, F32)
+    c1, c2, sd = coef[:, 0:1], coef[:, 1:2], coef[:, 2:3]
+    with np.errstate(all="ignore"):
+        mean = ((c1 * x_t).astype(F32) + (c2 * eps).astype(F32)).astype(F32)
+        nz = noise if add_noise else np.zeros_like(x_t)
+        return (mean + (sd * nz).astype(F32)).astype(F32)
+
+
+def add_noise(x0, noise, coef) -> np.ndarray:
+    coef = np.asarray(coef, F32)
+    return ((x0 * coef[:, 0:1]).astype(F32) + (noise * coef[:, 1:2]).astype(F32)).astype(F32)

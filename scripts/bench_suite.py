@@ -5,6 +5,9 @@ C2  int4 g128 dequant+GEMM, M = 2048 / 4096, K = N = 4096 (MFMA-bound) + M-sweep
 C2' standalone per-tensor quantize (min/max + quantize+pack) and dequant of an 8192x4096 f32 tensor
 C3  int2/int4 mixed 12-layer stack, seq 4096, d 4096
 C4  int4 KV quantize (K and V, per tensor) + dequant-attention, S 8192, 32 heads x 128
+C5  denoise loop: 12 int4 layers d 4096, seq 2048, 50 steps; per step the phase-aware KV cache
+    update (K,V [1, 2048, 4096] re-quantized at 8 and 4 bits) and p_sample fused into the last
+    layer's GEMM epilogue (one GPU; the multi-GPU forms are in parallel.py)
 Timings: HIP events on the launch stream over back-to-back launches (includes launch gaps);
 run under `rocprofv3 --kernel-trace --stats` for per-kernel durations.
 """
@@ -138,8 +141,31 @@ def c4():
          tflops=round(fl / s / 1e12, 1), mfma_frac=round(fl / s / PEAK, 3))
 
 
+def c5(steps=50):
+    dm, M, Lyr = 4096, 2048, 12
+    layers = [d.QuantLinear.from_weight(0.02 * torch.randn(dm, dm, device=dev), None, 4, 128) for _ in range(Lyr)]
+    cfg = d.DiffusionConfig(num_timesteps=steps, hidden_size=dm, num_layers=Lyr)
+    K = torch.randn(1, M, dm, device=dev)
+    V = torch.randn(1, M, dm, device=dev)
+    kv = d.KVCacheEntry.new(K, V, cfg.prefill_bits, cfg.decode_bits)
+    loop = d.DenoiseLoop(layers, cfg, cumprod=d.Cumprod.INCLUSIVE, seed=1, kv_cache=kv)
+    x = torch.randn(M, dm, device=dev)
+    loop.sample(x, 2)                      # warm-up (workspaces, coefficient cache)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    out = loop.sample(x, steps)
+    e1.record()
+    torch.cuda.synchronize()
+    s = e0.elapsed_time(e1) * 1e-3
+    fl = steps * Lyr * 2 * M * dm * dm
+    emit(config="C5 denoise loop 12 x int4 d4096, seq 2048, 50 steps (KV update + fused p_sample)",
+         ms_total=round(s * 1e3, 2), ms_per_step=round(s / steps * 1e3, 3), tok_per_s_per_step=round(M / (s / steps)),
+         gemm_tflops=round(fl / s / 1e12, 1), finite=bool(torch.isfinite(out).all()))
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["c1", "c2", "c2p", "c3", "c4"]
+    which = sys.argv[1:] or ["c1", "c2", "c2p", "c3", "c4", "c5"]
     prewarm()
     for w in which:
         globals()[w]()

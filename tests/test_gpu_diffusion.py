@@ -1,0 +1,166 @@
+"""GPU parity of the diffusion-step kernels against the C oracle: the seeded
+noise stream, p_sample and add_noise bit for bit, the GEMM-fused p_sample epilogue bit-identical
+to the unfused pair on every GEMM path, the phase-aware KV cache, and the denoise loop against
+an f32 torch restatement."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    return np.asarray(a, np.float32).view(np.uint32)
+
+
+def same(a, b):
+    a, b = np.asarray(a, np.float32), np.asarray(b, np.float32)
+    return ((bits(a) == bits(b)) | (np.isnan(a) & np.isnan(b))).all()
+
+
+@pytest.mark.parametrize("seed,offset,n", [(0, 0, 1 << 20), (1234, 4, 4099), (2**63 + 7, 1 << 40, 77), (5, 8, 3)])
+def test_randn_bit_exact(dllm, cuda, orc, seed, offset, n):
+    import torch
+    z = dllm.randn(n, seed, offset).cpu().numpy()
+    assert np.array_equal(bits(z), bits(orc.randn(seed, offset, n)))
+
+
+@pytest.mark.parametrize("B,D", [(6, 64), (3, 1001), (1, 4096 * 33)])
+@pytest.mark.parametrize("cumprod", [0, 1])
+def test_p_sample_bit_exact(dllm, cuda, orc, B, D, cumprod):
+    import torch
+    cfg = dllm.DiffusionConfig(num_timesteps=1000)
+    rng = np.random.default_rng(B * D)
+    x = rng.standard_normal((B, D)).astype(np.float32)
+    eps = rng.standard_normal((B, D)).astype(np.float32)
+    t = [999, 0, 1, 500, 2, 3][:B]
+    coef = orc.p_sample_coeffs(cfg.create_beta_schedule(), t, cumprod)
+    flag = t[0] > 0
+    # generated noise (seeded stream, offset 8)
+    y = dllm.p_sample(cfg, torch.from_numpy(x), t, torch.from_numpy(eps), seed=77, offset=8,
+                      cumprod=dllm.Cumprod(cumprod)).cpu().numpy()
+    ref = orc.p_sample(x, eps, orc.randn(77, 8, B * D).reshape(B, D), coef, add_noise=flag)
+    assert same(y, ref)
+    # caller-supplied noise
+    nz = rng.standard_normal((B, D)).astype(np.float32)
+    y2 = dllm.p_sample(cfg, torch.from_numpy(x), t, torch.from_numpy(eps), noise=torch.from_numpy(nz),
+                       cumprod=dllm.Cumprod(cumprod)).cpu().numpy()
+    assert same(y2, orc.p_sample(x, eps, nz, coef, add_noise=flag))
+
+
+def test_p_sample_last_step_without_noise(dllm, cuda, orc):
+    """t[0] == 0: the reference adds zeros (lib.rs:1198-1204); inclusive form, finite result."""
+    import torch
+    cfg = dllm.DiffusionConfig()
+    x = np.random.default_rng(1).standard_normal((2, 128)).astype(np.float32)
+    e = np.random.default_rng(2).standard_normal((2, 128)).astype(np.float32)
+    y = dllm.p_sample(cfg, torch.from_numpy(x), [0, 0], torch.from_numpy(e), seed=3,
+                      cumprod=dllm.Cumprod.INCLUSIVE).cpu().numpy()
+    coef = orc.p_sample_coeffs(cfg.create_beta_schedule(), [0, 0], inclusive=True)
+    assert same(y, orc.p_sample(x, e, None, coef, add_noise=False)) and np.isfinite(y).all()
+
+
+@pytest.mark.parametrize("cumprod", [0, 1])
+def test_add_noise_bit_exact(dllm, cuda, orc, cumprod):
+    import torch
+    cfg = dllm.DiffusionConfig()
+    rng = np.random.default_rng(11)
+    x0 = rng.standard_normal((4, 515)).astype(np.float32)
+    t = [0, 10, 999, 2000]
+    noisy, nz = dllm.add_noise(cfg, torch.from_numpy(x0), t, seed=9, offset=4, cumprod=dllm.Cumprod(cumprod))
+    ref_nz = orc.randn(9, 4, x0.size).reshape(x0.shape)
+    assert np.array_equal(bits(nz.cpu().numpy()), bits(ref_nz))
+    coef = orc.add_noise_coeffs(cfg.create_beta_schedule(), t, cumprod)
+    assert same(noisy.cpu().numpy(), orc.add_noise(x0, ref_nz, coef))
+    n2, _ = dllm.add_noise(cfg, torch.from_numpy(x0), t, noise=torch.from_numpy(ref_nz), cumprod=dllm.Cumprod(cumprod))
+    assert same(n2.cpu().numpy(), orc.add_noise(x0, ref_nz, coef))
+
+
+# (M, K, N, rows_per_sample): decode path (unfused), split-K (fused in the combine), 128-row ring,
+# 256x128 ring, 256x256 ring -- all with the fused entry point vs forward(f32) + p_sample.
+@pytest.mark.parametrize("M,K,N,rps", [(48, 512, 256, 16), (256, 1024, 4096, 64), (1024, 256, 4096, 1024),
+                                       (2048, 256, 4096, 512), (4096, 256, 4096, 4096)])
+def test_linear_psample_fused_bit_identical(dllm, cuda, M, K, N, rps):
+    import torch
+    g = torch.Generator(device="cuda").manual_seed(M + K)
+    W = 0.05 * torch.randn(K, N, device="cuda", generator=g)
+    b = 0.1 * torch.randn(N, device="cuda", generator=g)
+    lin = dllm.QuantLinear.from_weight(W, b, 4, 128)
+    X = torch.randn(M, K, device="cuda", generator=g).half()
+    xt = torch.randn(M, N, device="cuda", generator=g)
+    S = M // rps
+    cfg = dllm.DiffusionConfig()
+    t = [999 - 7 * i for i in range(S)]
+    coef_np, flag = dllm.diffusion.p_sample_coeffs(cfg, t, S, dllm.Cumprod.INCLUSIVE)
+    coef = torch.from_numpy(coef_np).cuda()
+    fused = lin.forward_psample(X, xt, coef, rps, flag, seed=5, offset=16)
+    eps = lin(X, out_dtype=torch.float32)
+    ref = torch.empty_like(xt)
+    row_coef = coef.repeat_interleave(rps, dim=0).contiguous()
+    lib = dllm._lib.load()
+    dllm._lib.check(lib.dllm_p_sample(C.c_void_p(xt.data_ptr()), C.c_void_p(eps.data_ptr()), None,
+                                      C.c_void_p(row_coef.data_ptr()), M, N, int(flag), 5, 16,
+                                      C.c_void_p(ref.data_ptr()), C.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    torch.cuda.synchronize()
+    assert torch.equal(fused.view(torch.int32), ref.view(torch.int32))
+    # in place (x_prev aliases x_t)
+    xt2 = xt.clone()
+    lin.forward_psample(X, xt2, coef, rps, flag, seed=5, offset=16, out=xt2)
+    assert torch.equal(xt2.view(torch.int32), ref.view(torch.int32))
+    lin.close()
+
+
+def test_kv_cache_entry_phases(dllm, cuda, orc):
+    import torch
+    rng = np.random.default_rng(3)
+    K = rng.standard_normal((1, 64, 256)).astype(np.float32)
+    V = rng.standard_normal((1, 64, 256)).astype(np.float32)
+    c = dllm.KVCacheEntry.new(torch.from_numpy(K).cuda(), torch.from_numpy(V).cuda(), 8, 4)
+    assert c.is_prefill_phase and c.get_current_quant_bits() == 8 and len(c) == 64
+    q, s, z = orc.quantize_tensor(K, 8)
+    assert np.array_equal(bits(c.get_keys().cpu().numpy().ravel()), bits(orc.dequantize_tensor(q, s, z)))
+    c.set_phase(False)
+    assert c.get_current_quant_bits() == 4
+    q, s, z = orc.quantize_tensor(V, 4)
+    assert np.array_equal(bits(c.get_values().cpu().numpy().ravel()), bits(orc.dequantize_tensor(q, s, z)))
+    # lib.rs:279-302 accounting: packed K+V at 8 and at 4 bits
+    n = K.size
+    assert c.memory_usage() == 2 * n + 2 * ((n * 4 + 7) // 8)
+    K2 = K + 1.0
+    c.update(torch.from_numpy(K2).cuda(), torch.from_numpy(V).cuda())
+    q, s, z = orc.quantize_tensor(K2, 4)
+    assert np.array_equal(bits(c.get_keys().cpu().numpy().ravel()), bits(orc.dequantize_tensor(q, s, z)))
+
+
+def test_denoise_loop_vs_torch_f32(dllm, cuda, orc):
+    """A 3-layer loop (d = 512, M = 256 tokens, 6 steps, inclusive alpha-bar) against the same
+    recursion in torch f32 on the exported dequantized weights, f16 activations between layers
+    and the oracle's noise stream: tolerance 2e-3 relative on the final state."""
+    import torch
+    d, M, L, steps = 512, 256, 3, 6
+    g = torch.Generator(device="cuda").manual_seed(0)
+    Ws = [0.04 * torch.randn(d, d, device="cuda", generator=g) for _ in range(L)]
+    layers = [dllm.QuantLinear.from_weight(W, None, 4, 128) for W in Ws]
+    cfg = dllm.DiffusionConfig(num_timesteps=steps, beta_start=0.01, beta_end=0.2)
+    loop = dllm.DenoiseLoop(layers, cfg, cumprod=dllm.Cumprod.INCLUSIVE, seed=21)
+    x0 = torch.randn(M, d, device="cuda", generator=g)
+    out = loop.sample(x0.clone(), steps)
+    Wh = []
+    for lin in layers:
+        codes, s, z = lin.export()
+        cd = orc.unpack_bits(codes.cpu().numpy(), d * d, 4).reshape(d, d)
+        Wh.append(torch.from_numpy(orc.dequantize_weights(cd, s.cpu().numpy(), z.cpu().numpy(), 128)).cuda())
+    x = x0.clone()
+    for i, t in enumerate(range(steps - 1, -1, -1)):
+        h = x
+        for j, W in enumerate(Wh):
+            h = h.half().float() @ W
+            if j < L - 1:
+                h = h.half().float()
+        coef, flag = dllm.diffusion.p_sample_coeffs(cfg, [t], 1, dllm.Cumprod.INCLUSIVE)
+        c1, c2, sd = (float(v) for v in coef[0])
+        nz = torch.from_numpy(orc.randn(21, i * M * d, M * d).reshape(M, d)).cuda() if flag else 0.0
+        x = (c1 * x + c2 * h) + sd * nz
+    rel = (torch.linalg.norm(out - x) / torch.linalg.norm(x)).item()
+    assert rel <= 2e-3, rel
