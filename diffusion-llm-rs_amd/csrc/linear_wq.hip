@@ -65,6 +65,7 @@ struct PSampleEpi {
     int add;
     uint64_t seed, offset;
     float *x_prev;
+    const float *noise;   // precomputed noise [M][N] (e.g. drawn on a side stream), or null: in-lane
 };
 
 // Four consecutive outputs (m, n..n+3) of the fused epilogue; N % 4 == 0, offset % 4 == 0.
@@ -74,7 +75,14 @@ __device__ __forceinline__ void psample4(const PSampleEpi &e, int m, int n, int 
     const float *c = e.coef + 3 * (m / e.rps);
     const float c1 = c[0], c2 = c[1], sd = c[2];
     float z[4] = {0.f, 0.f, 0.f, 0.f};
-    if (e.add) rng::normal4(e.seed, (e.offset + i) / 4, z);
+    if (e.add) {
+        if (e.noise) {
+            const float4 nv = *reinterpret_cast<const float4 *>(e.noise + i);
+            z[0] = nv.x; z[1] = nv.y; z[2] = nv.z; z[3] = nv.w;
+        } else {
+            rng::normal4(e.seed, (e.offset + i) / 4, z);
+        }
+    }
     const float4 x = *reinterpret_cast<const float4 *>(e.x_t + i);
     float4 o;
     o.x = (c1 * x.x + c2 * e0) + sd * z[0];
@@ -613,7 +621,6 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
     const unsigned kt0 = static_cast<unsigned>(ks) * nk;
     const unsigned kpg = static_cast<unsigned>(group) / kBK;
     const unsigned nt = static_cast<unsigned>(n0 + cw * 32) >> 5;
-    const int ncol = n0 + cw * 32 + (lane & 31);
 
     // X: kXRounds rounds of kWT KiB (kWT waves x 64 lanes x 16 B); round i, wave w covers rows
     // 8 (kWT i + w) .. +8.
@@ -628,7 +635,11 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
         xsrc[i] = X + static_cast<size_t>(grow) * K + c * 8;
     }
     const uint32_t *wsrc = wdev + (static_cast<size_t>(nt) * nk_all * 64 + lane) * BITS;
-    const uint32_t *szsrc = sz + ncol;
+    // Scales: one 16-B LDS-DMA per block per k-step (wave szw; 4 columns per lane) instead of one
+    // 256-B DMA per wave: each LDS-DMA costs its wave ~60-185 issue cycles whatever its size.
+    const int szw = KG == 1 ? 0 : NW;
+    const bool has_w = KG == 1 || kg == 0, has_sz = wave == szw;
+    const uint32_t *szsrc = sz + n0 + 4 * (lane & (8 * NW - 1));
 
     const uint32_t wv = static_cast<uint32_t>(wave), cwv = static_cast<uint32_t>(cw);
     // A stage is kXRounds + 2 pieces: X rounds, the weight words, the scale dword (pieces a wave
@@ -645,7 +656,7 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
         }
         if constexpr (LAB & 2) return;
         if (p == SL::kXRounds) {
-            if (KG == 1 || kg == 0) {
+            if (has_w) {
                 const uint32_t *wp = wsrc + static_cast<size_t>(kt) * 64 * BITS;
                 const uint32_t wb = base + SL::kX + cwv * (64 * BITS * 4);
                 if constexpr (BITS == 4) {
@@ -658,8 +669,8 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
                     glds4_asm(wp + 1, wb + 256);
                 }
             }
-        } else if (KG == 1 || kg == 1) {
-            glds4_asm(szsrc + (kt / kpg) * Npad, base + SL::kX + SL::kW + cwv * 256);
+        } else if (has_sz) {
+            glds16_asm(szsrc + (kt / kpg) * Npad, base + SL::kX + SL::kW);
         }
     };
     auto stage = [&](uint8_t *sb, unsigned kt) {
@@ -668,8 +679,10 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
     };
     // Counted wait leaving the newest stage's DMAs (this wave's own count) in flight.
     auto wait_prev = [&]() {
-        if (KG == 1 || kg == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kOps0) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kOps1) : "memory");
+        if (has_w && has_sz) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kXRounds + SL::kWOps + 1) : "memory");
+        else if (has_w) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kXRounds + SL::kWOps) : "memory");
+        else if (has_sz) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kXRounds + 1) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kXRounds) : "memory");
     };
 
     float16_t acc[MR];
@@ -688,7 +701,14 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
         soff[j] = (lane & 31) * (kBK * 2) + ((((2 * s + hsel) ^ rowx)) << 4);
     }
 
+    half8_t bconst = half8_t{(_Float16)lane, 1, 1, 1, 1, 1, 1, (_Float16)wave};
+    asm volatile("" : "+v"(bconst));
     auto read_b = [&](half8_t (&b)[MR], const uint8_t *sb, int j) {
+        if constexpr (LAB & 8) {   // measurement only: loop-invariant B fragments, no LDS reads
+#pragma unroll
+            for (int r = 0; r < MR; ++r) b[r] = bconst;
+            return;
+        }
 #pragma unroll
         for (int r = 0; r < MR; ++r) b[r] = *reinterpret_cast<const half8_t *>(sb + soff[j] + r * 32 * kBK * 2);
     };
@@ -699,7 +719,15 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
     // Compute stage `sb`; stage `pf` receives k-step kt+2.
     auto step = [&](const uint8_t *sb, uint8_t *pf, unsigned kt) {
         const bool issue = kt + 2 < nk;
-        if (issue) stage(pf, kt + 2);
+        if (!(LAB & 32) && issue) stage(pf, kt + 2);
+        if constexpr (LAB & 4) {   // measurement only: the ring and its waits without any compute
+            if (issue) wait_prev();
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+            return;
+        }
         uint32_t w[BITS];
         lds_words<BITS>(w, sb + SL::kX + cw * (64 * BITS * 4), lane);
         if constexpr (KG == 2) {
@@ -708,9 +736,13 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
             for (int i = 0; i < BITS / 2; ++i) w[i] = kg ? w[BITS / 2 + i] : w[i];
         }
         half2_t nz, sc;
-        split_sz(*reinterpret_cast<const uint32_t *>(sb + SL::kX + SL::kW + cw * 256 + lane * 4), nz, sc);
+        split_sz(*reinterpret_cast<const uint32_t *>(sb + SL::kX + SL::kW + (cw * 32 + (lane & 31)) * 4), nz, sc);
         half8_t bA[MR], bB[MR];
         read_b(bA, sb, 0);
+        if constexpr (LAB & 32) {   // measurement: head-of-step LDS reads drained before the DMAs issue
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (issue) stage(pf, kt + 2);
+        }
         half8_t aA = dequant_frag<BITS>(w, 0, nz, sc), aB;
         auto sub = [&](half8_t (&bc)[MR], half8_t (&bn)[MR], const half8_t &ac, half8_t &an, int j) {
             __builtin_amdgcn_sched_barrier(0);
@@ -736,7 +768,7 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
             sub(bB, bA, aB, aA, 3);
         }
         // Stage kt+1 must have landed; kt+2's DMAs may stay in flight across the barrier.
-        if (issue) wait_prev();
+        if (issue && !(LAB & 16)) wait_prev();
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
@@ -846,6 +878,214 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
             for (int qd = 0; qd < 4; ++qd)
                 store_out4<YT>(yrow, bias, nb0 + 8 * qd, N, vec_ok, acc[r][4 * qd + 0], acc[r][4 * qd + 1],
                                acc[r][4 * qd + 2], acc[r][4 * qd + 3]);
+        }
+    }
+}
+
+// 256 x 256 ring GEMM with the 2 (m) x 4 (n) wave layout: wave (rm, cg) = (wave / 4, wave % 4) owns
+// rows m0 + 128 rm .. +128 (4 m-reps) and columns n0 + 64 cg .. +64 (two 32-column fragments), so
+// each B fragment read from LDS feeds two MFMAs (half the LDS read traffic of the 1 x 8 layout of
+// wq_gemm8_kernel<8, 8>, which measured its DMA ring serialised behind the fragment reads) for
+// twice the dequant VALU per MFMA.  Stage layout and LDS-DMA pattern are those of
+// wq_gemm8_kernel<NW = 8, MR = 8>: wave w stages X rounds, weight fragment w and its scales.
+template <int BITS, typename YT, bool SPLIT = false, int EPI = 0>
+__global__ void __launch_bounds__(512, 1)
+wq_gemm_w2_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdev,
+                  const uint32_t *__restrict__ sz, const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad,
+                  int group, int nbm, int nbn, int nsplit = 1, float *__restrict__ ws = nullptr,
+                  PSampleEpi epi = PSampleEpi{}) {
+    using SL = StageLayout8<BITS, 8, 8, 1>;
+    constexpr int kRep = 4, kFr = 2;
+    __shared__ __attribute__((aligned(16))) uint8_t st0[SL::kBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t st1[SL::kBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t st2[SL::kBytes];
+
+    const int nb = nbm * nbn * nsplit, orig = blockIdx.x;
+    const int xcd = orig % kXCDs, q8 = nb / kXCDs, r8 = nb % kXCDs;
+    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / kXCDs;
+    const int ks = wgid / (nbm * nbn), tile = wgid % (nbm * nbn);
+    const int bm = tile / nbn, bn = tile % nbn;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int rm = wave >> 2, cg = wave & 3;
+    const int m0 = bm * 256, n0 = bn * 256;
+    const unsigned nk_all = static_cast<unsigned>(K) / kBK;
+    const unsigned nk = nk_all / static_cast<unsigned>(nsplit);
+    const unsigned kt0 = static_cast<unsigned>(ks) * nk;
+    const unsigned kpg = static_cast<unsigned>(group) / kBK;
+
+    // Staging (as wq_gemm8_kernel<8, 8>): wave w loads X rounds, weight fragment w, scales of w.
+    const int chunk_st = lane & 7;
+    const __half *xsrc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int row = (i * 8 + wave) * 8 + (lane >> 3);
+        int grow = m0 + row;
+        grow = grow < M ? grow : M - 1;
+        const int c = chunk_st ^ ((row >> 1) & 7);
+        xsrc[i] = X + static_cast<size_t>(grow) * K + c * 8;
+    }
+    const unsigned ntw = static_cast<unsigned>(n0 + wave * 32) >> 5;
+    const uint32_t *wsrc = wdev + (static_cast<size_t>(ntw) * nk_all * 64 + lane) * BITS;
+    const uint32_t *szsrc = sz + n0 + wave * 32 + (lane & 31);
+    const uint32_t wv = static_cast<uint32_t>(wave);
+    auto stage = [&](uint8_t *sb, unsigned kt) {
+        const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(sb));
+        kt += kt0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) glds16_asm(xsrc[i] + kt * kBK, base + wv * 1024 + i * 8192);
+        const uint32_t *wp = wsrc + static_cast<size_t>(kt) * 64 * BITS;
+        const uint32_t wb = base + SL::kX + wv * (64 * BITS * 4);
+        if constexpr (BITS == 4) {
+            glds16_asm(wp, wb);
+        } else if constexpr (BITS == 8) {
+            glds16_asm(wp, wb);
+            glds16_asm(wp + 4, wb + 64 * 16);
+        } else {
+            glds4_asm(wp, wb);
+            glds4_asm(wp + 1, wb + 256);
+        }
+        glds4_asm(szsrc + (kt / kpg) * Npad, base + SL::kX + SL::kW + wv * 256);
+    };
+
+    float16_t acc[kFr][kRep];
+#pragma unroll
+    for (int f = 0; f < kFr; ++f)
+#pragma unroll
+        for (int r = 0; r < kRep; ++r)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[f][r][e] = 0.0f;
+
+    const int hsel = lane >> 5;
+    const int rowx = ((lane & 31) >> 1) & 7;
+    int soff[4];
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) soff[s2] = (rm * 128 + (lane & 31)) * (kBK * 2) + ((((2 * s2 + hsel) ^ rowx)) << 4);
+
+    auto read_b = [&](half8_t (&b)[kRep], const uint8_t *sb, int s2) {
+#pragma unroll
+        for (int r = 0; r < kRep; ++r) b[r] = *reinterpret_cast<const half8_t *>(sb + soff[s2] + r * 32 * kBK * 2);
+    };
+    auto step = [&](const uint8_t *sb, uint8_t *pf, unsigned kt) {
+        const bool issue = kt + 2 < nk;
+        if (issue) stage(pf, kt + 2);
+        uint32_t w[kFr][BITS];
+        half2_t nz[kFr], sc[kFr];
+#pragma unroll
+        for (int f = 0; f < kFr; ++f) {
+            const int fr = 2 * cg + f;
+            lds_words<BITS>(w[f], sb + SL::kX + fr * (64 * BITS * 4), lane);
+            split_sz(*reinterpret_cast<const uint32_t *>(sb + SL::kX + SL::kW + fr * 256 + lane * 4), nz[f], sc[f]);
+        }
+        half8_t bA[kRep], bB[kRep];
+        half8_t aA[kFr], aB[kFr];
+        read_b(bA, sb, 0);
+#pragma unroll
+        for (int f = 0; f < kFr; ++f) aA[f] = dequant_frag<BITS>(w[f], 0, nz[f], sc[f]);
+        auto sub = [&](half8_t (&bc)[kRep], half8_t (&bn)[kRep], const half8_t (&ac)[kFr], half8_t (&an)[kFr], int s2) {
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_setprio(1);
+            if (s2 < 3) {
+                read_b(bn, sb, s2 + 1);
+#pragma unroll
+                for (int f = 0; f < kFr; ++f) an[f] = dequant_frag<BITS>(w[f], s2 + 1, nz[f], sc[f]);
+            }
+#pragma unroll
+            for (int f = 0; f < kFr; ++f)
+#pragma unroll
+                for (int r = 0; r < kRep; ++r)
+                    acc[f][r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac[f], bc[r], acc[f][r], 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < kFr * kRep; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                if (i < kRep) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+            }
+            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        sub(bA, bB, aA, aB, 0);
+        sub(bB, bA, aB, aA, 1);
+        sub(bA, bB, aA, aB, 2);
+        sub(bB, bA, aB, aA, 3);
+        if (issue) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kOps0) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    stage(st0, 0);
+    if (nk > 1) stage(st1, 1);
+    if (nk > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kOps0) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    for (unsigned kt = 0; kt < nk; kt += 3) {
+        step(st0, st2, kt);
+        if (kt + 1 < nk) step(st1, st0, kt + 1);
+        if (kt + 2 < nk) step(st2, st1, kt + 2);
+    }
+
+    // Epilogue: acc[f][r] reg e -> n = n0 + 32 (2 cg + f) + (e&3) + 8 (e>>2) + 4 hsel,
+    //                              m = m0 + 128 rm + 32 r + (lane&31).
+#pragma unroll
+    for (int f = 0; f < kFr; ++f) {
+        const int nb0 = n0 + (2 * cg + f) * 32 + 4 * hsel;
+        if constexpr (SPLIT) {
+            float *slab = ws + static_cast<size_t>(ks) * M * Npad;
+#pragma unroll
+            for (int r = 0; r < kRep; ++r) {
+                const int m = m0 + rm * 128 + r * 32 + (lane & 31);
+                if (m >= M) continue;
+                float *prow = slab + static_cast<size_t>(m) * Npad + nb0;
+#pragma unroll
+                for (int qd = 0; qd < 4; ++qd)
+                    *reinterpret_cast<float4 *>(prow + 8 * qd) = make_float4(
+                        acc[f][r][4 * qd + 0], acc[f][r][4 * qd + 1], acc[f][r][4 * qd + 2], acc[f][r][4 * qd + 3]);
+            }
+            continue;
+        }
+        float4 bv[4];
+#pragma unroll
+        for (int qd = 0; qd < 4; ++qd) bv[qd] = *reinterpret_cast<const float4 *>(bias + nb0 + 8 * qd);
+        if constexpr (EPI == 1) {
+#pragma unroll
+            for (int r = 0; r < kRep; ++r) {
+                const int m = m0 + rm * 128 + r * 32 + (lane & 31);
+                if (m >= M) continue;
+#pragma unroll
+                for (int qd = 0; qd < 4; ++qd) {
+                    if (nb0 + 8 * qd >= N) continue;
+                    psample4(epi, m, nb0 + 8 * qd, N, acc[f][r][4 * qd + 0] + bv[qd].x, acc[f][r][4 * qd + 1] + bv[qd].y,
+                             acc[f][r][4 * qd + 2] + bv[qd].z, acc[f][r][4 * qd + 3] + bv[qd].w);
+                }
+            }
+            continue;
+        }
+        const bool full = (m0 + 256 <= M) && (n0 + 256 <= N) && (N % 4) == 0;
+        if (full) {
+#pragma unroll
+            for (int r = 0; r < kRep; ++r) {
+                YT *yrow = Y + static_cast<size_t>(m0 + rm * 128 + r * 32 + (lane & 31)) * N + nb0;
+#pragma unroll
+                for (int qd = 0; qd < 4; ++qd)
+                    store4<YT>(yrow + 8 * qd, acc[f][r][4 * qd + 0] + bv[qd].x, acc[f][r][4 * qd + 1] + bv[qd].y,
+                               acc[f][r][4 * qd + 2] + bv[qd].z, acc[f][r][4 * qd + 3] + bv[qd].w);
+            }
+        } else {
+            const bool vec_ok = (N % 4) == 0;
+#pragma unroll
+            for (int r = 0; r < kRep; ++r) {
+                const int m = m0 + rm * 128 + r * 32 + (lane & 31);
+                if (m >= M) continue;
+                YT *yrow = Y + static_cast<size_t>(m) * N;
+#pragma unroll
+                for (int qd = 0; qd < 4; ++qd)
+                    store_out4<YT>(yrow, bias, nb0 + 8 * qd, N, vec_ok, acc[f][r][4 * qd + 0], acc[f][r][4 * qd + 1],
+                                   acc[f][r][4 * qd + 2], acc[f][r][4 * qd + 3]);
+            }
         }
     }
 }
@@ -1104,15 +1344,18 @@ int launch_ring(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t
     const unsigned nb = static_cast<unsigned>(nbm * nbn * nsplit);
     const PSampleEpi ep = epi ? *epi : PSampleEpi{};
     if (EPI == 0 && h->rlab != 0 && nsplit == 1) {   // measurement only
-        if (h->rlab == 1)
-            wq_gemm8_kernel<BITS, YT, NW, MR, false, KG, 1><<<nb, NW * KG * 64, 0, st>>>(
-                X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn);
-        else if (h->rlab == 2)
-            wq_gemm8_kernel<BITS, YT, NW, MR, false, KG, 2><<<nb, NW * KG * 64, 0, st>>>(
-                X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn);
-        else
-            wq_gemm8_kernel<BITS, YT, NW, MR, false, KG, 3><<<nb, NW * KG * 64, 0, st>>>(
-                X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn);
+        switch (h->rlab) {
+#define DLLM_RLAB(L)                                                                                              \
+    case L:                                                                                                       \
+        wq_gemm8_kernel<BITS, YT, NW, MR, false, KG, L><<<nb, NW * KG * 64, 0, st>>>(                           \
+            X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn);   \
+        break;
+            DLLM_RLAB(1) DLLM_RLAB(2) DLLM_RLAB(3) DLLM_RLAB(4) DLLM_RLAB(5) DLLM_RLAB(6) DLLM_RLAB(7)
+            DLLM_RLAB(8) DLLM_RLAB(9) DLLM_RLAB(10) DLLM_RLAB(11) DLLM_RLAB(16) DLLM_RLAB(20) DLLM_RLAB(32)
+            DLLM_RLAB(40)
+#undef DLLM_RLAB
+            default: break;
+        }
         DLLM_LAUNCH_CHECK();
         return DLLM_OK;
     }
@@ -1142,8 +1385,18 @@ int launch_auto(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t
                 const PSampleEpi *epi = nullptr) {
     const int np = static_cast<int>(h->Npad);
     const int mb256 = (M + 255) / 256, mb128 = (M + 127) / 128;
-    if (np % 256 == 0 && mb256 * (np / 256) >= kCUs) return launch_ring<BITS, YT, 8, 8, 1, EPI>(h, X, M, Y, st, 1, epi);
-    const bool kg2 = h->variant == 4;   // variant 5: the same tiles with one k-group (A/B)
+    if (np % 256 == 0 && mb256 * (np / 256) >= kCUs) {
+        if (h->variant == 7) {
+            const PSampleEpi ep = epi ? *epi : PSampleEpi{};
+            wq_gemm_w2_kernel<BITS, YT, false, EPI><<<static_cast<unsigned>(mb256 * (np / 256)), 512, 0, st>>>(
+                X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, mb256, np / 256,
+                1, nullptr, ep);
+            DLLM_LAUNCH_CHECK();
+            return DLLM_OK;
+        }
+        return launch_ring<BITS, YT, 8, 8, 1, EPI>(h, X, M, Y, st, 1, epi);
+    }
+    const bool kg2 = h->variant != 5;   // variant 5: the same tiles with one k-group (A/B)
     if (mb256 * (np / 128) >= kCUs)
         return kg2 ? launch_ring<BITS, YT, 4, 8, 2, EPI>(h, X, M, Y, st, 1, epi)
                    : launch_ring<BITS, YT, 4, 8, 1, EPI>(h, X, M, Y, st, 1, epi);
@@ -1158,7 +1411,7 @@ int launch_auto(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t
 template <int BITS, typename YT>
 int launch_gemm_t(const dllm_linear *h, const __half *X, size_t M, YT *Y, hipStream_t st) {
     if (M <= static_cast<size_t>(kDecodeMaxM)) return launch_decode<BITS, YT>(h, X, M, Y, st);
-    if (h->variant == 4 || h->variant == 5) return launch_auto<BITS, YT>(h, X, (int)M, Y, st);
+    if (h->variant == 4 || h->variant == 5 || h->variant == 7) return launch_auto<BITS, YT>(h, X, (int)M, Y, st);
     if (h->variant == 6) {   // previous policy: 2-stage kernels, 128-row tiles + split below 256 tiles
         const int tiles256 = static_cast<int>((M + kBM - 1) / kBM) * static_cast<int>(h->Npad / kBN);
         if (tiles256 < kCUs) return launch_mid<BITS, YT>(h, X, (int)M, Y, st);
@@ -1333,7 +1586,7 @@ int dllm_linear_forward(dllm_linear_t h, const void *X, size_t M, int x_dtype, v
 
 int dllm_linear_forward_psample(dllm_linear_t h, const void *X, size_t M, int x_dtype, const float *x_t,
                                 const float *coef, size_t rows_per_sample, int add_noise, uint64_t seed,
-                                uint64_t offset, float *x_prev, dllm_stream_t stream) {
+                                uint64_t offset, const float *noise, float *x_prev, dllm_stream_t stream) {
     if (!h) return fail(DLLM_ERR_INVALID_PARAMS, "null handle");
     if (x_dtype != DLLM_F32 && x_dtype != DLLM_F16) return fail(DLLM_ERR_UNSUPPORTED, "x_dtype");
     if (M == 0) return DLLM_OK;
@@ -1341,12 +1594,13 @@ int dllm_linear_forward_psample(dllm_linear_t h, const void *X, size_t M, int x_
     if (M > (1u << 30)) return fail(DLLM_ERR_SHAPE_MISMATCH, "M too large");
     if (h->N % 4) return fail(DLLM_ERR_UNSUPPORTED, "fused p_sample needs N % 4 == 0");
     if (offset % 4) return fail(DLLM_ERR_INVALID_PARAMS, "offset must be a multiple of 4");
-    if ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(x_t) | reinterpret_cast<uintptr_t>(x_prev)) & 15)
-        return fail(DLLM_ERR_INVALID_PARAMS, "X, x_t and x_prev must be 16-byte aligned");
+    if ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(x_t) | reinterpret_cast<uintptr_t>(x_prev) |
+         reinterpret_cast<uintptr_t>(noise)) & 15)
+        return fail(DLLM_ERR_INVALID_PARAMS, "X, x_t, noise and x_prev must be 16-byte aligned");
     hipStream_t st = as_stream(stream);
     const __half *Xh = nullptr;
     if (const int rc = prepare_x(h, X, M, x_dtype, st, &Xh)) return rc;
-    if (M <= static_cast<size_t>(kDecodeMaxM) || (h->variant != 4 && h->variant != 5)) {
+    if (M <= static_cast<size_t>(kDecodeMaxM) || (h->variant != 4 && h->variant != 5 && h->variant != 7)) {
         // Paths without the fused epilogue: f32 eps through a per-stream workspace, then p_sample
         // (the same eps bits, hence the same result as the fused form on that path).
         float *eps = splitk_workspace(st, M * h->N * sizeof(float), 1);
@@ -1366,9 +1620,9 @@ int dllm_linear_forward_psample(dllm_linear_t h, const void *X, size_t M, int x_
             DLLM_LAUNCH_CHECK();
             coef = rc3;
         }
-        return dllm_p_sample(x_t, eps, nullptr, coef, M, h->N, add_noise, seed, offset, x_prev, stream);
+        return dllm_p_sample(x_t, eps, noise, coef, M, h->N, add_noise, seed, offset, x_prev, stream);
     }
-    const PSampleEpi ep{x_t, coef, static_cast<int>(rows_per_sample), add_noise ? 1 : 0, seed, offset, x_prev};
+    const PSampleEpi ep{x_t, coef, static_cast<int>(rows_per_sample), add_noise ? 1 : 0, seed, offset, x_prev, noise};
     switch (h->bits) {
     case 2: return psample_fused<2>(h, Xh, (int)M, ep, st);
     case 4: return psample_fused<4>(h, Xh, (int)M, ep, st);
@@ -1408,11 +1662,11 @@ int dllm_linear_set_kernel_variant(dllm_linear_t h, int variant) {
         h->dlab = variant - 16;
         return DLLM_OK;
     }
-    if (variant >= 32 && variant < 36) {   // ring-kernel ablation mask (measurement only)
+    if (variant >= 32 && variant < 96) {   // ring-kernel ablation mask (measurement only)
         h->rlab = variant - 32;
         return DLLM_OK;
     }
-    if (variant < 0 || variant > 6) return fail(DLLM_ERR_INVALID_PARAMS, "variant must be 0..6 (16..23: decode ablation)");
+    if (variant < 0 || variant > 7) return fail(DLLM_ERR_INVALID_PARAMS, "variant must be 0..7 (16..23, 32..47: ablations)");
     h->variant = variant;
     h->dlab = h->rlab = 0;
     return DLLM_OK;

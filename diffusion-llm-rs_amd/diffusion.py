@@ -246,18 +246,26 @@ class DenoiseLoop:
     (dllm_linear_forward_psample); a layer callable without that entry point (e.g. a
     tensor-parallel pair whose output is all-reduced) is followed by the p_sample kernel.
     x is [M, d] f32 for one sample of M = seq tokens (the reference's [batch, hidden*seq] row
-    laid out token-major); the noise of step i is stream elements [i M d, (i+1) M d)."""
+    laid out token-major); the noise of step i is stream elements [i M d, (i+1) M d).
+
+    overlap=True runs the work of a step that does not depend on x -- the KV-cache update (the
+    simple model's update_kv_cache passes K/V through, lib.rs:826-835, and forward_with_cache
+    ignores them, :815-824) and the step's noise draw (dllm_randn into one of two buffers) -- on
+    a side stream while layers 0..L-2 run; the last layer waits only for its noise.  The result
+    is bit-identical to overlap=False."""
 
     def __init__(self, layers: Sequence, config: DiffusionConfig, cumprod: Cumprod = Cumprod.INCLUSIVE,
                  alpha_mode: AlphaMode = AlphaMode.PER_SAMPLE, seed: int = 0,
-                 kv_cache: Optional[KVCacheEntry] = None):
+                 kv_cache: Optional[KVCacheEntry] = None, overlap: bool = True):
         self.layers = list(layers)
         self.config = config
         self.cumprod, self.alpha_mode, self.seed = cumprod, alpha_mode, seed
         self.kv_cache = kv_cache
-        betas = config.create_beta_schedule()
-        self._betas = betas
+        self.overlap = overlap
+        self._betas = config.create_beta_schedule()
         self._coef_cache = {}
+        self._side = None
+        self._noise = None
 
     def _coef(self, t: int) -> tuple[torch.Tensor, bool]:
         if t not in self._coef_cache:
@@ -269,7 +277,8 @@ class DenoiseLoop:
             self._coef_cache[t] = (torch.from_numpy(coef).cuda(), bool(flag.value))
         return self._coef_cache[t]
 
-    def step(self, x: torch.Tensor, t: int, step_index: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def step(self, x: torch.Tensor, t: int, step_index: int, out: Optional[torch.Tensor] = None,
+             noise: Optional[torch.Tensor] = None, noise_ready: Optional[torch.cuda.Event] = None) -> torch.Tensor:
         M, d = x.shape
         coef, flag = self._coef(t)
         offset = step_index * M * d
@@ -278,12 +287,14 @@ class DenoiseLoop:
             h = layer(h, out_dtype=torch.float16)
         last = self.layers[-1]
         out = torch.empty_like(x) if out is None else out
+        if noise_ready is not None:
+            torch.cuda.current_stream().wait_event(noise_ready)
         if hasattr(last, "forward_psample"):
-            last.forward_psample(h, x, coef, M, flag, self.seed, offset, out)
+            last.forward_psample(h, x, coef, M, flag, self.seed, offset, out, noise=noise)
         else:
             eps = last(h, out_dtype=torch.float32)
-            check(_lib.load().dllm_p_sample(_ptr(x), _ptr(eps), None, _ptr(coef), 1, M * d, int(flag), self.seed,
-                                            offset, _ptr(out), _stream()))
+            check(_lib.load().dllm_p_sample(_ptr(x), _ptr(eps), None if noise is None else _ptr(noise), _ptr(coef),
+                                            1, M * d, int(flag), self.seed, offset, _ptr(out), _stream()))
         return out
 
     def kv_step(self, t: int, num_steps: int):
@@ -307,8 +318,34 @@ class DenoiseLoop:
         num_steps = num_steps or self.config.num_timesteps
         x = x.to(device="cuda", dtype=torch.float32).contiguous()
         buf = torch.empty_like(x)
+        M, d = x.shape
+        main = torch.cuda.current_stream()
+        if not self.overlap:
+            for i, t in enumerate(range(num_steps - 1, -1, -1)):
+                self.kv_step(t, num_steps)
+                buf = self.step(x, t, i, out=buf)
+                x, buf = buf, x
+            return x
+        if self._side is None:
+            self._side = torch.cuda.Stream()
+        if self._noise is None or self._noise[0].shape != x.shape:
+            self._noise = [torch.empty_like(x), torch.empty_like(x)]
+        side = self._side
+        freed = [None, None]        # main-stream events: noise buffer j no longer read
+        side.wait_stream(main)
         for i, t in enumerate(range(num_steps - 1, -1, -1)):
-            self.kv_step(t, num_steps)
-            buf = self.step(x, t, i, out=buf)
+            j = i % 2
+            nz = self._noise[j]
+            with torch.cuda.stream(side):
+                if freed[j] is not None:
+                    side.wait_event(freed[j])
+                check(_lib.load().dllm_randn(self.seed, i * M * d, _ptr(nz), M * d, _stream()))
+                ready = torch.cuda.Event()
+                ready.record(side)
+                self.kv_step(t, num_steps)
+            buf = self.step(x, t, i, out=buf, noise=nz, noise_ready=ready)
+            freed[j] = torch.cuda.Event()
+            freed[j].record(main)
             x, buf = buf, x
+        main.wait_stream(side)
         return x

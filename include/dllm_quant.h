@@ -227,11 +227,13 @@ int dllm_add_noise(const float *x0, const float *noise, const float *coef, size_
 /* Denoiser output layer fused with p_sample: eps = X . W^ + b (f32, as dllm_linear_forward with
  * y_dtype DLLM_F32) feeds x_prev = (c1 x_t + c2 eps) + std * n in the GEMM epilogue, with x_t and
  * x_prev f32 [M][N] (device, may alias), coef device [M / rows_per_sample][3] (row m uses
- * sample m / rows_per_sample) and n = stream element offset + m N + n.  Bit-identical to
- * dllm_linear_forward(..., DLLM_F32) followed by dllm_p_sample.  N % 4 == 0. */
+ * sample m / rows_per_sample) and n = noise[m][n] when noise != NULL (f32 [M][N], e.g. drawn by
+ * dllm_randn on a side stream while the earlier layers run), else stream element offset + m N + n
+ * generated in the epilogue.  Bit-identical to dllm_linear_forward(..., DLLM_F32) followed by
+ * dllm_p_sample with the same noise.  N % 4 == 0. */
 int dllm_linear_forward_psample(dllm_linear_t h, const void *X, size_t M, int x_dtype, const float *x_t,
                                 const float *coef, size_t rows_per_sample, int add_noise, uint64_t seed,
-                                uint64_t offset, float *x_prev, dllm_stream_t stream);
+                                uint64_t offset, const float *noise, float *x_prev, dllm_stream_t stream);
 
 /* ---- host-slice variants (synchronous; stage through device memory; not graph-capturable) ----
  * The literal shapes of the reference's Rust signatures, for callers holding host slices. */

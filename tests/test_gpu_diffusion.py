@@ -164,3 +164,25 @@ def test_denoise_loop_vs_torch_f32(dllm, cuda, orc):
         x = (c1 * x + c2 * h) + sd * nz
     rel = (torch.linalg.norm(out - x) / torch.linalg.norm(x)).item()
     assert rel <= 2e-3, rel
+
+
+def test_denoise_loop_overlap_bit_identical(dllm, cuda):
+    """The side-stream schedule (noise drawn ahead, KV update concurrent) gives the same bits as the
+    serial loop, and the KV cache ends in the same state."""
+    import torch
+    d, M, L, steps = 256, 192, 2, 5
+    g = torch.Generator(device="cuda").manual_seed(4)
+    layers = [dllm.QuantLinear.from_weight(0.04 * torch.randn(d, d, device="cuda", generator=g), None, 4, 128)
+              for _ in range(L)]
+    cfg = dllm.DiffusionConfig(num_timesteps=steps, beta_start=0.01, beta_end=0.2)
+    x0 = torch.randn(M, d, device="cuda", generator=g)
+    K = torch.randn(1, 64, d, device="cuda", generator=g)
+    outs, kvs = [], []
+    for overlap in (False, True):
+        kv = dllm.KVCacheEntry.new(K.clone(), K.clone() * 2, 8, 4)
+        loop = dllm.DenoiseLoop(layers, cfg, cumprod=dllm.Cumprod.INCLUSIVE, seed=3, kv_cache=kv, overlap=overlap)
+        outs.append(loop.sample(x0.clone(), steps))
+        kvs.append(kv.get_keys())
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
+    assert torch.equal(kvs[0], kvs[1])

@@ -397,15 +397,16 @@ def test_host_entry_points(dllm, orc):
 
 
 def test_gemm_variants_bit_identical(dllm, torch):
-    """All prefill schedules (0..3: 256x128 tile; 4: 256x256 tile, 3-stage LDS ring) accumulate in
-    the same k order, so they must agree bit for bit -- including a ragged M tail."""
+    """All prefill schedules (0..3: 256x128 tile; 4: 256x256 tile, 3-stage LDS ring, 1x8 waves;
+    7: the same tile with 2x4 waves) accumulate every output in the same k order, so they must
+    agree bit for bit -- including a ragged M tail."""
     K, N, M = 1024, 4096, 4352
     g = torch.Generator(device="cuda").manual_seed(8)
     W = 0.02 * torch.randn(K, N, device="cuda", generator=g)
     X = torch.randn(M, K, device="cuda", generator=g).half()
     lin = dllm.QuantLinear.from_weight(W, 0.1 * torch.randn(N, device="cuda", generator=g), 4, 128)
     outs = {}
-    for v in (0, 3, 4):
+    for v in (0, 3, 4, 7):
         lin.set_kernel_variant(v)
         outs[v] = lin(X, out_dtype=torch.float32)
-    assert torch.equal(outs[0], outs[3]) and torch.equal(outs[0], outs[4])
+    assert torch.equal(outs[0], outs[3]) and torch.equal(outs[0], outs[4]) and torch.equal(outs[0], outs[7])
