@@ -11,13 +11,15 @@ this package is the host-side mirror of the reference's Rust operator surface:
 * ``kvquant``      -- ``prefill_kvquant_rs::kvquant`` (BitQuantizer, PrefillKVQuant, SystemConfig)
   and ``diffusion_prefill``'s compress/decompress_vector.
 * ``linear``       -- the int2/int4/int8 group-quantized linear layer (dequant + MFMA GEMM).
+* ``serde``        -- bincode / serde_json wire formats of QuantizationParams, QuantizedTensor and
+  the diffusion_prefill CompressedVector hand-off record.
 * ``diffusion``    -- ``diffuse_llm``'s schedules, add_noise / p_sample (seeded device noise), the
   phase-aware KVCacheEntry and the denoise loop (last layer fused with p_sample).
 """
 from . import _lib
-from ._lib import (CalibrationRequired, HipError, InvalidParams, QuantizationError, ShapeMismatch,
-                   UnsupportedOperation)
-from . import quantization, quant, kvquant, linear, parallel, diffusion
+from ._lib import (CalibrationRequired, HipError, InvalidParams, QuantizationError, SerializationError,
+                   ShapeMismatch, UnsupportedOperation)
+from . import quantization, quant, kvquant, linear, parallel, diffusion, serde
 from .quantization import (QuantizedKVCacheEntry, QuantizedTensor, compression_ratio, dequantize_tensor, kv_attention,
                            pack, quantize_tensor, unpack)
 from .quant import CalibrationData, DefaultQuantizer, QuantizationParams, QuantizationType, quant_utils

@@ -59,9 +59,14 @@ class HipError(QuantizationError):
     code = ERR_HIP
 
 
+class SerializationError(QuantizationError, ValueError):
+    """QuantizationError::Serialization (quantization/src/error.rs:29-30, from bincode / serde_json)."""
+    code = ERR_SERIALIZATION
+
+
 _ERRORS = {ERR_INVALID_PARAMS: InvalidParams, ERR_UNSUPPORTED: UnsupportedOperation,
            ERR_SHAPE_MISMATCH: ShapeMismatch, ERR_CALIBRATION_REQUIRED: CalibrationRequired,
-           ERR_HIP: HipError, ERR_NO_DEVICE: HipError}
+           ERR_SERIALIZATION: SerializationError, ERR_HIP: HipError, ERR_NO_DEVICE: HipError}
 
 P, S, U8, I32, U32, FL, INT = (C.c_void_p, C.c_size_t, C.c_uint8, C.c_int32, C.c_uint32, C.c_float, C.c_int)
 U64 = C.c_uint64
