@@ -12,14 +12,23 @@
 // Layout: Q, O f16 [S][H][D]; K, V codes in the canonical packed bitstream of the flattened
 // [S][H][D] tensor (one per-tensor {scale, zp} pair each, on the device), D = 128.
 // Workgroup = 8 waves = 256 queries of one head; every 64-key block of K and V is staged once in
-// LDS (K as [key][d], V transposed as [d][key]) and shared by the 8 waves; two LDS buffers, one
-// barrier per block: block j+1's codes are loaded before block j's MFMAs and written to the other
-// buffer after them.
+// LDS (K as [key][d], V transposed as [d][key]) and shared by the 8 waves.
 // Per wave (32 queries): S^T = K Q^T with 32x32x16 f16 MFMA (keys in registers, the query on the
 // lane, so the softmax row reductions are lane-local plus one cross-half shuffle), then O = P V with
 // the S^T accumulator converted in place to the A operand (no LDS round trip for P).  The O rescale
 // is skipped when no query's running max moved (exact: the factor is then 1).
+// Software pipeline: iteration kb issues S^T of block kb+1 on the matrix pipe and runs the
+// softmax of block kb on the VALU meanwhile, then P V of block kb.  K is therefore staged two
+// blocks ahead and V one block ahead, each in its own two-buffer ring; one barrier per block; no
+// buffer is written in the iteration that reads it.
+// Dequantize once (v4): every (head, 64-key block) of K and V is unpacked to the exact f16 (q - z)
+// image of its LDS tiles ONCE, by kv_stage_kernel, into a workspace; the attention loop then
+// streams those images into LDS with LDS-DMA (no VALU).  Unpacking inside the attention loop
+// repeated it for each of a head's S/256 query workgroups (32x at S = 8192) and cost ~30 % of the
+// kernel (measured by ablation: DLLM_ATTN_LAB=2).
 #include "common.hpp"
+
+#include <cstdlib>
 
 typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
 typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
@@ -36,14 +45,18 @@ constexpr int kQT = 32 * kWaves; // queries per workgroup
 constexpr int kKRow = kD + 8;    // K row stride (halves): 272 B, conflict-free b128 fragment reads
 constexpr int kVRow = kKB + 8;   // Vt row stride (halves): 144 B
 
-struct AttnBuf {
-    _Float16 k[kKB][kKRow];       // 17 KiB
-    _Float16 vt[kD][kVRow];       // 18 KiB
-};
 struct AttnSmem {
-    AttnBuf buf[2];
+    _Float16 k[2][kKB][kKRow];    // 2 x 17 KiB
+    _Float16 vt[2][kD][kVRow];    // 2 x 18 KiB
     float bcast[kWaves][32];      // per-wave per-query factors (alpha, then 1/l)
 };
+
+// Workspace image of one (head, key block): the K tile then the transposed V tile, byte for byte
+// the LDS layout (row padding included), so one 1-KiB LDS-DMA piece per wave-instruction moves it.
+constexpr int kKImg = kKB * kKRow * 2;          // 17408 B = 17 pieces
+constexpr int kVImg = kD * kVRow * 2;           // 18432 B = 18 pieces
+constexpr int kImg = kKImg + kVImg;
+static_assert(kKImg % 1024 == 0 && kVImg % 1024 == 0, "images must be whole 1-KiB DMA pieces");
 
 // Codes of one thread's share of a block, loaded to registers ahead of the MFMAs.
 // K: thread t < 256 owns key t>>2, dims 32*(t&3) .. +32 (one row chunk).
@@ -53,30 +66,32 @@ struct Raw {
     uint32_t w[BITS == 4 ? 4 : 8];
 };
 
+// 32-bit byte offsets through buffer resources: keys at or past S read as 0 (out of range, no
+// memory access) instead of being clamped, and no 64-bit address math per block.
 template <int BITS>
-__device__ __forceinline__ void load_raw(Raw<BITS> &r, const uint8_t *__restrict__ Kq, const uint8_t *__restrict__ Vq,
-                                         int tid, int j0, int S, int H, int h) {
+__device__ __forceinline__ void load_raw(Raw<BITS> &r, __amdgpu_buffer_rsrc_t krs, __amdgpu_buffer_rsrc_t vrs,
+                                         int tid, int jk, int jv, int H, int h) {
+    constexpr int kRowB = kD * BITS / 8;   // packed bytes per (key, head) row
     if (tid < 256) {
         const int key = tid >> 2, d0 = 32 * (tid & 3);
-        const int s = min(j0 + key, S - 1);
-        const size_t e = (static_cast<size_t>(s) * H + h) * kD + d0;
+        const uint32_t off = static_cast<uint32_t>(((jk + key) * H + h) * kRowB + d0 * BITS / 8);
         if constexpr (BITS == 4) {
-            const uint4 v = *reinterpret_cast<const uint4 *>(Kq + e / 2);   // 32 codes
+            const uint4 v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(krs, off, 0, 0));
             r.w[0] = v.x; r.w[1] = v.y; r.w[2] = v.z; r.w[3] = v.w;
         } else {
-            const uint4 a = *reinterpret_cast<const uint4 *>(Kq + e), b = *reinterpret_cast<const uint4 *>(Kq + e + 16);
+            const uint4 a = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(krs, off, 0, 0));
+            const uint4 b = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(krs, off + 16, 0, 0));
             r.w[0] = a.x; r.w[1] = a.y; r.w[2] = a.z; r.w[3] = a.w; r.w[4] = b.x; r.w[5] = b.y; r.w[6] = b.z; r.w[7] = b.w;
         }
     } else {
         const int t = tid - 256, k4 = 4 * (t >> 4), d0 = 8 * (t & 15);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int s = min(j0 + k4 + i, S - 1);
-            const size_t e = (static_cast<size_t>(s) * H + h) * kD + d0;
+            const uint32_t off = static_cast<uint32_t>(((jv + k4 + i) * H + h) * kRowB + d0 * BITS / 8);
             if constexpr (BITS == 4) {
-                r.w[i] = *reinterpret_cast<const uint32_t *>(Vq + e / 2);          // 8 codes
+                r.w[i] = __builtin_amdgcn_raw_buffer_load_b32(vrs, off, 0, 0);
             } else {
-                const uint2 v = *reinterpret_cast<const uint2 *>(Vq + e);
+                const uint2 v = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(vrs, off, 0, 0));
                 r.w[2 * i] = v.x; r.w[2 * i + 1] = v.y;
             }
         }
@@ -94,7 +109,8 @@ __device__ __forceinline__ half2_t pair_qz(uint32_t lo_word_codes, int shift, ha
 }
 
 template <int BITS>
-__device__ __forceinline__ void store_raw(const Raw<BITS> &r, AttnBuf &b, int tid, half2_t kz, half2_t vz) {
+__device__ __forceinline__ void store_raw(const Raw<BITS> &r, _Float16 (&bk)[kKB][kKRow], _Float16 (&bvt)[kD][kVRow],
+                                          int tid, half2_t kz, half2_t vz) {
     constexpr int CPW = 32 / BITS;   // codes per word
     if (tid < 256) {
         const int key = tid >> 2, d0 = 32 * (tid & 3);
@@ -108,7 +124,7 @@ __device__ __forceinline__ void store_raw(const Raw<BITS> &r, AttnBuf &b, int ti
                 out[2 * p] = v[0];
                 out[2 * p + 1] = v[1];
             }
-            *reinterpret_cast<half8_t *>(&b.k[key][d0 + 8 * g]) = out;
+            *reinterpret_cast<half8_t *>(&bk[key][d0 + 8 * g]) = out;
         }
     } else {
         const int t = tid - 256, k4 = 4 * (t >> 4), d0 = 8 * (t & 15);
@@ -125,24 +141,48 @@ __device__ __forceinline__ void store_raw(const Raw<BITS> &r, AttnBuf &b, int ti
             }
 #pragma unroll
         for (int dd = 0; dd < 8; ++dd)   // transposed: 4 consecutive keys of one dim per 8-B store
-            *reinterpret_cast<half4_t *>(&b.vt[d0 + dd][k4]) = half4_t{v[0][dd], v[1][dd], v[2][dd], v[3][dd]};
+            *reinterpret_cast<half4_t *>(&bvt[d0 + dd][k4]) = half4_t{v[0][dd], v[1][dd], v[2][dd], v[3][dd]};
     }
 }
 
+// Pre-pass: unpack block kb of head h to its LDS image (through LDS, so the stores to the
+// workspace are coalesced 16-B rows).  Keys past S read as code 0 (buffer range check); the
+// attention kernel masks their scores and their P is 0.
 template <int BITS>
+__global__ void __launch_bounds__(512) kv_stage_kernel(const uint8_t *__restrict__ Kq, const float *__restrict__ kp,
+                                                      const uint8_t *__restrict__ Vq, const float *__restrict__ vp,
+                                                      int S, int H, int nkb, uint8_t *__restrict__ img) {
+    __shared__ __attribute__((aligned(16))) _Float16 tk[kKB][kKRow];
+    __shared__ __attribute__((aligned(16))) _Float16 tv[kD][kVRow];
+    const int tid = threadIdx.x, kb = blockIdx.x, h = blockIdx.y;
+    const _Float16 nkz = static_cast<_Float16>(-(1024.0f + kp[1]));
+    const _Float16 nvz = static_cast<_Float16>(-(1024.0f + vp[1]));
+    const half2_t kz{nkz, nkz}, vz{nvz, nvz};
+    const int nbytes = static_cast<int>(static_cast<size_t>(S) * H * kD * BITS / 8);
+    const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(Kq), 0, nbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(Vq), 0, nbytes, 0x00020000);
+    Raw<BITS> raw;
+    load_raw<BITS>(raw, krs, vrs, tid, kb * kKB, kb * kKB, H, h);
+    store_raw<BITS>(raw, tk, tv, tid, kz, vz);
+    __syncthreads();
+    uint8_t *dst = img + (static_cast<size_t>(h) * nkb + kb) * kImg;
+    const uint4 *sk = reinterpret_cast<const uint4 *>(&tk[0][0]);
+    const uint4 *sv = reinterpret_cast<const uint4 *>(&tv[0][0]);
+    for (int i = tid; i < kKImg / 16; i += 512) reinterpret_cast<uint4 *>(dst)[i] = sk[i];
+    for (int i = tid; i < kVImg / 16; i += 512) reinterpret_cast<uint4 *>(dst + kKImg)[i] = sv[i];
+}
+
+template <int LAB = 0>
 __global__ void __launch_bounds__(kWaves * 64)
-kv_attention_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__ Kq, const float *__restrict__ kp,
-                    const uint8_t *__restrict__ Vq, const float *__restrict__ vp, int S, int H,
-                    _Float16 *__restrict__ O) {
+kv_attention_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__ img, const float *__restrict__ kp,
+                    const float *__restrict__ vp, int S, int H, _Float16 *__restrict__ O) {
+    const int nkb = (S + kKB - 1) / kKB;
     __shared__ __attribute__((aligned(16))) AttnSmem sm;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int h = blockIdx.y;
     const int q0 = blockIdx.x * kQT + wave * 32;
     const int ql = lane & 31, hh = lane >> 5;
     const float ks = kp[0], vs = vp[0];
-    const _Float16 nkz = static_cast<_Float16>(-(1024.0f + kp[1]));   // zp is an integer <= 255: exact
-    const _Float16 nvz = static_cast<_Float16>(-(1024.0f + vp[1]));
-    const half2_t kz{nkz, nkz}, vz{nvz, nvz};
     // exp2 domain, K scale folded in: p = exp2(c * raw - m), c = log2(e) * s_k / sqrt(D).
     const float c = 1.4426950408889634f * ks / sqrtf(static_cast<float>(kD));
 
@@ -162,52 +202,97 @@ kv_attention_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__ 
         for (int e = 0; e < 16; ++e) o[dt][e] = 0.0f;
     float m_run = -INFINITY, l_run = 0.0f;   // for query q0 + ql (same in both lane halves)
 
-    const int nkb = (S + kKB - 1) / kKB;
-    Raw<BITS> raw;
-    load_raw<BITS>(raw, Kq, Vq, tid, 0, S, H, h);
-    store_raw<BITS>(raw, sm.buf[0], tid, kz, vz);
-    __syncthreads();
-
-    for (int kb = 0; kb < nkb; ++kb) {
-        const int j0 = kb * kKB;
-        AttnBuf &cur = sm.buf[kb & 1];
-        const bool more = kb + 1 < nkb;
-        if (more) load_raw<BITS>(raw, Kq, Vq, tid, j0 + kKB, S, H, h);   // in flight during the MFMAs
-
-        // ---- S^T (2 x 32 keys x 32 queries) = (q_k - z_k) Q^T ----
-        float16_t st[2];
+    // S^T (2 x 32 keys x 32 queries) of a staged K block: st[u][r] is key 32u + (r&3) + 8(r>>2) + 4hh
+    // of the block, query q0 + ql.
+    auto qk = [&](float16_t (&st)[2], const _Float16 (&kb_)[kKB][kKRow]) {
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) st[u][e] = 0.0f;
 #pragma unroll
             for (int t = 0; t < kD / 16; ++t) {
-                const half8_t kf = *reinterpret_cast<const half8_t *>(&cur.k[32 * u + ql][16 * t + 8 * hh]);
+                const half8_t kf = *reinterpret_cast<const half8_t *>(&kb_[32 * u + ql][16 * t + 8 * hh]);
                 st[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[t], st[u], 0, 0, 0);
             }
         }
-        // st[u][r]: key = j0 + 32u + (r&3) + 8(r>>2) + 4 hh, query = q0 + ql.
+    };
+
+    // LDS-DMA of the workspace images: wave w moves pieces w, w + 8, ... (1 KiB each).
+    const uint8_t *himg = img + static_cast<size_t>(h) * nkb * kImg + lane * 16;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(wave);
+    auto dma_k = [&](int blk, int buf) {
+        const uint8_t *src = himg + static_cast<size_t>(blk) * kImg;
+        const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_addr(&sm.k[buf][0][0]));
+        for (uint32_t p = wv; p < kKImg / 1024; p += kWaves) glds16_asm(src + p * 1024, dst + p * 1024);
+    };
+    auto dma_v = [&](int blk, int buf) {
+        const uint8_t *src = himg + static_cast<size_t>(blk) * kImg + kKImg;
+        const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_addr(&sm.vt[buf][0][0]));
+        for (uint32_t p = wv; p < kVImg / 1024; p += kWaves) glds16_asm(src + p * 1024, dst + p * 1024);
+    };
+    // Prologue: K and V of block 0 and K of block 1 staged; S^T of block 0 computed.
+    dma_k(0, 0);
+    dma_v(0, 0);
+    if (nkb > 1) dma_k(1, 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    float16_t st[2], sn[2];
+    qk(st, sm.k[0]);
+
+    for (int kb = 0; kb < nkb; ++kb) {
+        const int j0 = kb * kKB;
+        const bool more1 = kb + 1 < nkb, more2 = kb + 2 < nkb;
+        // Images in flight during this block's math: K of block kb+2 into the K buffer block kb
+        // used (read last iteration), V of block kb+1 into the V buffer of block kb-1.
+        if (!(LAB & 2)) {
+            if (more2) dma_k(kb + 2, kb & 1);
+            if (more1) dma_v(kb + 1, (kb + 1) & 1);
+        }
+        // S^T of block kb+1 on the matrix pipe while the VALU runs the softmax of block kb.
+        if (more1) {
+            if constexpr (LAB & 8) {
+#pragma unroll
+                for (int u = 0; u < 2; ++u) sn[u] = st[u] * 0.5f;
+            } else {
+                qk(sn, sm.k[(kb + 1) & 1]);
+            }
+        }
+
+        if constexpr (LAB & 1) {   // measurement only: no softmax
+            float lsum = 0.0f;
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) lsum += st[u][r];
+            l_run += lsum;
+        } else {
         float mloc = -INFINITY;
-        const bool tail = j0 + kKB > S;
+        if (__builtin_expect(j0 + kKB > S, 0)) {   // last, partial block only (a real branch)
+            asm volatile("" ::: "memory");
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
+            for (int u = 0; u < 2; ++u)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                if (tail) {
+                for (int r = 0; r < 16; ++r) {
                     const int key = j0 + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * hh;
                     st[u][r] = key < S ? st[u][r] : -INFINITY;
                 }
-                mloc = fmaxf(mloc, st[u][r]);
-            }
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) mloc = fmaxf(mloc, st[u][r]);
         mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
         const float m_new = fmaxf(m_run, mloc * c);
-        const float alpha = exp2f(m_run - m_new);   // exactly 1 when the max did not move
+        // v_exp_f32 directly (exp2f's denormal-range fix-up costs 3-4 extra VALU per element; P
+        // values below 2^-126 are 0 in the f16 P anyway).  exp2(0) = 1 exactly: alpha is exactly 1
+        // when the max did not move.
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
         float lsum = 0.0f;
 #pragma unroll
         for (int u = 0; u < 2; ++u)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                st[u][r] = exp2f(fmaf(st[u][r], c, -m_new));
+                st[u][r] = __builtin_amdgcn_exp2f(fmaf(st[u][r], c, -m_new));
                 lsum += st[u][r];
             }
         lsum += __shfl_xor(lsum, 32, 64);
@@ -228,25 +313,36 @@ kv_attention_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__ 
                 }
             }
         }
+        }
         // ---- O += P (q_v - z_v): P^T accumulator as the A operand (k-step s: keys 16s..16s+15) ----
+        const auto &vt = sm.vt[kb & 1];
+        if constexpr (!(LAB & 4)) {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const int u = s >> 1, sl = s & 1;
+        for (int s2 = 0; s2 < 4; ++s2) {
+            const int u = s2 >> 1, sl = s2 & 1;
             half8_t pa;
 #pragma unroll
             for (int j = 0; j < 8; ++j) pa[j] = static_cast<_Float16>(st[u][8 * sl + j]);
 #pragma unroll
             for (int dt = 0; dt < kD / 32; ++dt) {
                 // element j <-> key 16s + 8(j>>2) + 4hh + (j&3), d = 32dt + ql
-                const _Float16 *vrow = &cur.vt[32 * dt + ql][16 * s + 4 * hh];
+                const _Float16 *vrow = &vt[32 * dt + ql][16 * s2 + 4 * hh];
                 const half4_t lo = *reinterpret_cast<const half4_t *>(vrow);
                 const half4_t hi = *reinterpret_cast<const half4_t *>(vrow + 8);
                 const half8_t vb = half8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
                 o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(pa, vb, o[dt], 0, 0, 0);
             }
         }
-        if (more) store_raw<BITS>(raw, sm.buf[(kb + 1) & 1], tid, kz, vz);
-        __syncthreads();   // next block staged; this block's buffer free for block kb+2
+        } else {
+#pragma unroll
+            for (int dt = 0; dt < kD / 32; ++dt) o[dt] += st[dt >> 1] * 0.25f;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (more1) {
+            st[0] = sn[0];
+            st[1] = sn[1];
+        }
     }
 
     // ---- normalise (1/l and the V scale) and store: o[dt][r] -> query q0 + (r&3) + 8(r>>2) + 4hh ----
@@ -280,17 +376,34 @@ extern "C" int dllm_kv_attention(const void *Q, const uint8_t *Kq, const float *
     if (bits != 4 && bits != 8) return fail(DLLM_ERR_UNSUPPORTED, "dllm_kv_attention: bits must be 4 or 8");
     if (S == 0 || H == 0) return DLLM_OK;
     if (!Q || !Kq || !Vq || !k_params || !v_params || !O) return fail(DLLM_ERR_INVALID_PARAMS, "null pointer");
-    if (S > (1u << 28) || H > 65535) return fail(DLLM_ERR_SHAPE_MISMATCH, "S or H too large");
+    if (S * H * D * bits / 8 >= (size_t{1} << 31) || H > 65535)
+        return fail(DLLM_ERR_SHAPE_MISMATCH, "K/V codes must stay below 2 GiB (32-bit buffer offsets)");
     if ((reinterpret_cast<uintptr_t>(Kq) & 15) || (reinterpret_cast<uintptr_t>(Vq) & 15) ||
         (reinterpret_cast<uintptr_t>(Q) & 15))
         return fail(DLLM_ERR_INVALID_PARAMS, "Q, K and V codes must be 16-byte aligned");
-    dim3 grid(static_cast<unsigned>((S + kQT - 1) / kQT), static_cast<unsigned>(H));
+    hipStream_t st = as_stream(stream);
+    const int nkb = static_cast<int>((S + kKB - 1) / kKB);
+    uint8_t *img = reinterpret_cast<uint8_t *>(device_workspace(st, static_cast<size_t>(H) * nkb * kImg, 8));
+    if (!img) return DLLM_ERR_HIP;
+    dim3 sgrid(static_cast<unsigned>(nkb), static_cast<unsigned>(H));
     if (bits == 4)
-        kv_attention_kernel<4><<<grid, kWaves * 64, 0, as_stream(stream)>>>(
-            static_cast<const _Float16 *>(Q), Kq, k_params, Vq, v_params, (int)S, (int)H, static_cast<_Float16 *>(O));
+        kv_stage_kernel<4><<<sgrid, 512, 0, st>>>(Kq, k_params, Vq, v_params, (int)S, (int)H, nkb, img);
     else
-        kv_attention_kernel<8><<<grid, kWaves * 64, 0, as_stream(stream)>>>(
-            static_cast<const _Float16 *>(Q), Kq, k_params, Vq, v_params, (int)S, (int)H, static_cast<_Float16 *>(O));
+        kv_stage_kernel<8><<<sgrid, 512, 0, st>>>(Kq, k_params, Vq, v_params, (int)S, (int)H, nkb, img);
+    DLLM_LAUNCH_CHECK();
+    dim3 grid(static_cast<unsigned>((S + kQT - 1) / kQT), static_cast<unsigned>(H));
+    // DLLM_ATTN_LAB (measurement only; results are garbage when set): 1 no softmax, 2 no K/V
+    // staging, 4 no PV MFMAs, 8 no QK MFMAs.
+    static const int lab = [] { const char *e = getenv("DLLM_ATTN_LAB"); return e ? atoi(e) : 0; }();
+    const _Float16 *Qh = static_cast<const _Float16 *>(Q);
+    _Float16 *Oh = static_cast<_Float16 *>(O);
+    switch (lab) {
+#define DLLM_ALAB(L) case L: kv_attention_kernel<L><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh); break;
+        DLLM_ALAB(1) DLLM_ALAB(2) DLLM_ALAB(3) DLLM_ALAB(4) DLLM_ALAB(5) DLLM_ALAB(6) DLLM_ALAB(7)
+        DLLM_ALAB(8) DLLM_ALAB(12) DLLM_ALAB(13) DLLM_ALAB(14) DLLM_ALAB(15)
+#undef DLLM_ALAB
+        default: kv_attention_kernel<0><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh); break;
+    }
     DLLM_LAUNCH_CHECK();
     return DLLM_OK;
 }

@@ -2,7 +2,10 @@
 #include <hip/hip_runtime.h>
 
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
+#include <tuple>
 
 #include "dllm_quant.h"
 
@@ -15,6 +18,34 @@ void set_error(const std::string &msg) { g_last_error = msg; }
 int fail(int code, const std::string &msg) {
     g_last_error = msg;
     return code;
+}
+
+float *device_workspace(hipStream_t st, size_t bytes, int slot) {
+    static std::mutex mu;
+    static std::map<std::tuple<int, hipStream_t, int>, std::pair<float *, size_t>> pool;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(mu);
+    auto &e = pool[{dev, st, slot}];
+    if (e.second >= bytes) return e.first;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(st, &cs);
+    if (cs != hipStreamCaptureStatusNone) {
+        fail(DLLM_ERR_HIP, "device workspace must be sized before stream capture (run the shape once first)");
+        return nullptr;
+    }
+    if (e.first) {
+        if (hipStreamSynchronize(st) != hipSuccess) return nullptr;
+        (void)hipFree(e.first);
+        e = {nullptr, 0};
+    }
+    float *p = nullptr;
+    if (hipMalloc(reinterpret_cast<void **>(&p), bytes) != hipSuccess) {
+        fail(DLLM_ERR_HIP, "hipMalloc of a device workspace failed");
+        return nullptr;
+    }
+    e = {p, bytes};
+    return p;
 }
 
 }  // namespace dllm

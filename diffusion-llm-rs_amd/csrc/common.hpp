@@ -32,6 +32,31 @@ int fail(int code, const std::string &msg);
 
 inline hipStream_t as_stream(dllm_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Grow-only device workspace, one per (device, stream, slot): launches on one stream run in order,
+// so every call on that stream can share it.  A growth waits for the stream first (queued kernels
+// may still use the old buffer) and is refused while the stream is being captured.  Returns null
+// (error set) on failure.
+float *device_workspace(hipStream_t st, size_t bytes, int slot = 0);
+
+typedef __attribute__((address_space(3))) void *lds_void_ptr;
+typedef __attribute__((address_space(1))) void *gbl_void_ptr;
+
+// LDS-DMA (global_load_lds) issued from inline asm: invisible to hipcc's waitcnt pass, so the only
+// waits on these loads are the counted vmcnt statements placed by hand (M0 written in the statement).
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+    return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_ptr)(const_cast<void *>(p))));
+}
+__device__ __forceinline__ void glds16_asm(const void *gsrc, uint32_t lds_dst) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+__device__ __forceinline__ void glds4_asm(const void *gsrc, uint32_t lds_dst) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+
 constexpr int kWave = 64;      // CDNA wavefront width
 constexpr int kCUs = 256;      // MI355X compute units (8 XCDs x 32)
 constexpr int kXCDs = 8;

@@ -29,8 +29,6 @@
 typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
 typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
 typedef float float16_t __attribute__((ext_vector_type(16)));
-typedef __attribute__((address_space(3))) void *lds_void_ptr;
-typedef __attribute__((address_space(1))) void *gbl_void_ptr;
 
 struct dllm_linear {
     size_t K = 0, N = 0, Npad = 0, G = 0, group = 0;
@@ -556,21 +554,6 @@ wq_gemm_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__res
 // ---------------------------------------------------------------------------------------------
 // LDS-DMA issued from inline asm: invisible to hipcc's waitcnt pass, so the only waits on these
 // loads are the counted vmcnt statements placed by hand (guide 5.7, M0 written in the statement).
-__device__ __forceinline__ uint32_t lds_addr(const void *p) {
-    return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_void_ptr)(const_cast<void *>(p))));
-}
-__device__ __forceinline__ void glds16_asm(const void *gsrc, uint32_t lds_dst) {
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
-}
-__device__ __forceinline__ void glds4_asm(const void *gsrc, uint32_t lds_dst) {
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
-}
-
-
 template <int BITS, int NW = 8, int MR = kMReps, int KG = 1>
 struct StageLayout8 {
     static constexpr int kWaves = NW * KG;
@@ -1276,37 +1259,6 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float *__restr
     }
 }
 
-// Split-K slab workspace, one per (device, stream): launches on one stream run in order, so every
-// layer on that stream can share it.  It only grows; a growth waits for the stream first (queued
-// kernels may still read the old one) and is refused while the stream is being captured.
-float *splitk_workspace(hipStream_t st, size_t bytes, int slot = 0) {
-    static std::mutex mu;
-    static std::map<std::tuple<int, hipStream_t, int>, std::pair<float *, size_t>> pool;
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    std::lock_guard<std::mutex> lk(mu);
-    auto &e = pool[{dev, st, slot}];
-    if (e.second >= bytes) return e.first;
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    (void)hipStreamIsCapturing(st, &cs);
-    if (cs != hipStreamCaptureStatusNone) {
-        fail(DLLM_ERR_HIP, "split-K workspace must be sized before stream capture (run the shape once first)");
-        return nullptr;
-    }
-    if (e.first) {
-        if (hipStreamSynchronize(st) != hipSuccess) return nullptr;
-        (void)hipFree(e.first);
-        e = {nullptr, 0};
-    }
-    float *p = nullptr;
-    if (hipMalloc(reinterpret_cast<void **>(&p), bytes) != hipSuccess) {
-        fail(DLLM_ERR_HIP, "hipMalloc of the split-K workspace failed");
-        return nullptr;
-    }
-    e = {p, bytes};
-    return p;
-}
-
 // Mid-M prefill (too few 256-row tiles to fill 256 CUs): 128-row tiles, and when even those are
 // too few, K split into nsplit slices (slab partials + splitk_reduce_kernel).
 template <int BITS, typename YT>
@@ -1324,7 +1276,7 @@ int launch_mid(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t 
         DLLM_LAUNCH_CHECK();
         return DLLM_OK;
     }
-    float *ws = splitk_workspace(st, static_cast<size_t>(nsplit) * M * h->Npad * sizeof(float));
+    float *ws = device_workspace(st, static_cast<size_t>(nsplit) * M * h->Npad * sizeof(float));
     if (!ws) return DLLM_ERR_HIP;
     wq_gemm_kernel<BITS, YT, 3, MR, true><<<nb, kThreads, 0, st>>>(
         X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn, nsplit, ws);
@@ -1366,7 +1318,7 @@ int launch_ring(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t
         DLLM_LAUNCH_CHECK();
         return DLLM_OK;
     }
-    float *ws = splitk_workspace(st, static_cast<size_t>(nsplit) * M * h->Npad * sizeof(float));
+    float *ws = device_workspace(st, static_cast<size_t>(nsplit) * M * h->Npad * sizeof(float));
     if (!ws) return DLLM_ERR_HIP;
     wq_gemm8_kernel<BITS, YT, NW, MR, true, KG><<<nb, NW * KG * 64, 0, st>>>(
         X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn, nsplit, ws);
@@ -1603,7 +1555,7 @@ int dllm_linear_forward_psample(dllm_linear_t h, const void *X, size_t M, int x_
     if (M <= static_cast<size_t>(kDecodeMaxM) || (h->variant != 4 && h->variant != 5 && h->variant != 7)) {
         // Paths without the fused epilogue: f32 eps through a per-stream workspace, then p_sample
         // (the same eps bits, hence the same result as the fused form on that path).
-        float *eps = splitk_workspace(st, M * h->N * sizeof(float), 1);
+        float *eps = device_workspace(st, M * h->N * sizeof(float), 1);
         if (!eps) return DLLM_ERR_HIP;
         int rc = DLLM_OK;
         switch (h->bits) {
@@ -1614,7 +1566,7 @@ int dllm_linear_forward_psample(dllm_linear_t h, const void *X, size_t M, int x_
         if (rc) return rc;
         // Per-row coefficients: expand the per-sample table when samples span several rows.
         if (rows_per_sample != 1) {
-            float *rc3 = splitk_workspace(st, M * 3 * sizeof(float), 2);
+            float *rc3 = device_workspace(st, M * 3 * sizeof(float), 2);
             if (!rc3) return DLLM_ERR_HIP;
             expand_coef_kernel<<<grid_for(M, 256, kCUs), 256, 0, st>>>(coef, M, rows_per_sample, rc3);
             DLLM_LAUNCH_CHECK();

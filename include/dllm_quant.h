@@ -178,7 +178,8 @@ int dllm_linear_destroy(dllm_linear_t h);
  * (diffuse-llm-rs/src/lib.rs:910-915).  Build-defined consumer: per head, bidirectional SDPA
  * O = softmax(Q K^T / sqrt(D)) V, with K,V given as per-tensor quantized codes (a1 layout,
  * packed, `bits` in {4, 8}) + device params {scale, zp} (a2 dequant fused into the kernel).
- * Q f16 [S][H][D], O f16 [S][H][D], D == 128. */
+ * Q f16 [S][H][D], O f16 [S][H][D], D == 128.  K/V are unpacked once per call into a grow-only
+ * per-stream workspace (H * ceil(S/64) * 35 KiB), allocated on the first call of a shape. */
 int dllm_kv_attention(const void *Q, const uint8_t *Kq, const float *k_params, const uint8_t *Vq,
                       const float *v_params, uint8_t bits, size_t S, size_t H, size_t D, void *O,
                       dllm_stream_t stream);
