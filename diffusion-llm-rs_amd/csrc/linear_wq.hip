@@ -36,6 +36,7 @@ struct dllm_linear {
     int device = 0;
     uint32_t *wdev = nullptr;     // prefill layout (32x32x16 fragments)
     uint32_t *wdec = nullptr;     // decode layout (16x16x32 fragments)
+    uint32_t *w16 = nullptr;      // 16x16x32 prefill layout (wq_gemm16_kernel)
     uint32_t *sz = nullptr;       // [G][Npad]
     uint32_t *canon = nullptr;    // canonical packed codes (u32-padded)
     float *scales = nullptr;      // [G][N]
@@ -154,6 +155,36 @@ __global__ void __launch_bounds__(256) build_fragments_kernel(const uint32_t *__
             }
             dst[w] = word;
         }
+    }
+}
+
+// Canonical -> 16x16x32 prefill layout: [32-column tile][k64 slab][lane][bits words], lane l,
+// "substep" S' = 2 f + s (f: 16-column half of the tile, s: 32-deep half of the slab), code j of
+// the lane's 8 = column 32 nt + 16 f + (l & 15), k = 64 slab + 32 s + 8 (l >> 4) + j; words and
+// pair positions as the 32x32x16 layout with S' in place of its substep.  One thread per (n, slab).
+__global__ void __launch_bounds__(256) build_fragments16_kernel(const uint32_t *__restrict__ canon, size_t K, size_t N,
+                                                                size_t Npad, int bits, uint32_t *__restrict__ w16) {
+    const size_t n = blockIdx.x * static_cast<size_t>(256) + threadIdx.x;
+    const size_t kt = blockIdx.y;
+    if (n >= Npad) return;
+    const size_t nk = K / 64, nt = n >> 5;
+    const int f = static_cast<int>((n >> 4) & 1);
+    const int ppw = 16 / bits;
+    for (int o = 0; o < 4; ++o) {
+        const size_t lane = (n & 15) + 16 * o;
+        uint32_t *dst = w16 + ((nt * nk + kt) * 64 + lane) * bits;
+        uint32_t words[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int s2 = 0; s2 < 2; ++s2) {
+            for (int v = 0; v < 4; ++v) {
+                const int P = (2 * f + s2) * 4 + v;
+                const size_t k = kt * 64 + 32 * s2 + 8 * o + 2 * v;
+                uint32_t lo = 0, hi = 0;
+                if (n < N) { lo = canon_code(canon, k, n, N, bits); hi = canon_code(canon, k + 1, n, N, bits); }
+                words[P / ppw] |= (lo << (bits * (P % ppw))) | (hi << (16 + bits * (P % ppw)));
+            }
+        }
+        // This thread owns exactly the words of S' = 2f, 2f+1: [8f / ppw, (8f + 8) / ppw).
+        for (int w = (8 * f) / ppw; w < (8 * f + 8) / ppw; ++w) dst[w] = words[w];
     }
 }
 
@@ -1073,6 +1104,179 @@ wq_gemm_w2_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__
     }
 }
 
+// 256 x 256 ring GEMM on the 16x16x32 MFMA (same tile, waves, LDS-DMA ring and staging as
+// wq_gemm8_kernel<8, 8>, weights in the w16 layout): wave w owns columns n0 + 32 w .. +32 as two
+// 16-column fragments f and all 256 rows as 16 m-reps of 16; a 64-deep k-step is 2 substeps of
+// 32, each 4 quarters of 8 MFMAs (2 f x 4 reps) with the next quarter's X fragments prefetched.
+// Accumulator acc[f][r] reg i: token m = m0 + 16 r + (lane & 15), column
+// n = n0 + 32 w + 16 f + 4 (lane >> 4) + i.  (On random data the 16x16x32 shape holds a higher
+// clock under DVFS than the 32x32x16 one at equal cycles per FLOP: MI355X_MICROARCH.md item 7.)
+typedef float float4_t16 __attribute__((ext_vector_type(4)));
+template <int BITS, typename YT, int EPI = 0>
+__global__ void __launch_bounds__(512, 1)
+wq_gemm16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ w16,
+                 const uint32_t *__restrict__ sz, const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad,
+                 int group, int nbm, int nbn, PSampleEpi epi = PSampleEpi{}) {
+    using SL = StageLayout8<BITS, 8, 8, 1>;
+    constexpr int kRep = 16;
+    __shared__ __attribute__((aligned(16))) uint8_t st0[SL::kBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t st1[SL::kBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t st2[SL::kBytes];
+
+    const int nb = nbm * nbn, orig = blockIdx.x;
+    const int xcd = orig % kXCDs, q8 = nb / kXCDs, r8 = nb % kXCDs;
+    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / kXCDs;
+    const int bm = wgid / nbn, bn = wgid % nbn;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int m0 = bm * 256, n0 = bn * 256;
+    const unsigned nk = static_cast<unsigned>(K) / kBK;
+    const unsigned kpg = static_cast<unsigned>(group) / kBK;
+
+    const int chunk_st = lane & 7;
+    const __half *xsrc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int row = (i * 8 + wave) * 8 + (lane >> 3);
+        int grow = m0 + row;
+        grow = grow < M ? grow : M - 1;
+        const int c = chunk_st ^ ((row >> 1) & 7);
+        xsrc[i] = X + static_cast<size_t>(grow) * K + c * 8;
+    }
+    const unsigned nt = static_cast<unsigned>(n0 + wave * 32) >> 5;
+    const uint32_t *wsrc = w16 + (static_cast<size_t>(nt) * nk * 64 + lane) * BITS;
+    const uint32_t *szsrc = sz + n0 + 4 * lane;   // 256 columns = 64 lanes x 16 B
+    const uint32_t wv = static_cast<uint32_t>(wave);
+    auto stage = [&](uint8_t *sb, unsigned kt) {
+        const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(sb));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) glds16_asm(xsrc[i] + kt * kBK, base + wv * 1024 + i * 8192);
+        const uint32_t *wp = wsrc + static_cast<size_t>(kt) * 64 * BITS;
+        const uint32_t wb = base + SL::kX + wv * (64 * BITS * 4);
+        if constexpr (BITS == 4) {
+            glds16_asm(wp, wb);
+        } else if constexpr (BITS == 8) {
+            glds16_asm(wp, wb);
+            glds16_asm(wp + 4, wb + 64 * 16);
+        } else {
+            glds4_asm(wp, wb);
+            glds4_asm(wp + 1, wb + 256);
+        }
+        if (wave == 0) glds16_asm(szsrc + (kt / kpg) * Npad, base + SL::kX + SL::kW);
+    };
+    auto wait_prev = [&]() {
+        if (wave == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 + SL::kWOps + 1) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 + SL::kWOps) : "memory");
+    };
+
+    float4_t16 acc[2][kRep];
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int r = 0; r < kRep; ++r) acc[f][r] = float4_t16{0.f, 0.f, 0.f, 0.f};
+
+    // X fragment (B operand): lane reads row 16 r + (lane & 15), k chunk 4 s + (lane >> 4), swizzled
+    // by the row's (row >> 1) & 7 (the same for every r: conflict-free in each 16-lane group).
+    const int rl = lane & 15;
+    int soff[2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) soff[s2] = rl * (kBK * 2) + (((4 * s2 + (lane >> 4)) ^ ((rl >> 1) & 7)) << 4);
+    auto read_b4 = [&](half8_t (&b)[4], const uint8_t *sb, int s2, int q) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            b[i] = *reinterpret_cast<const half8_t *>(sb + soff[s2] + (4 * q + i) * 16 * kBK * 2);
+    };
+
+    auto step = [&](const uint8_t *sb, uint8_t *pf, unsigned kt) {
+        const bool issue = kt + 2 < nk;
+        if (issue) stage(pf, kt + 2);
+        uint32_t w[BITS];
+        lds_words<BITS>(w, sb + SL::kX + wave * (64 * BITS * 4), lane);
+        half2_t nz[2], sc[2];
+#pragma unroll
+        for (int f = 0; f < 2; ++f)
+            split_sz(*reinterpret_cast<const uint32_t *>(sb + SL::kX + SL::kW + (wave * 32 + 16 * f + rl) * 4), nz[f],
+                     sc[f]);
+        half8_t a0[2], a1[2];
+#pragma unroll
+        for (int f = 0; f < 2; ++f) a0[f] = dequant_frag<BITS>(w, 2 * f + 0, nz[f], sc[f]);
+        half8_t bA[4], bB[4];
+        read_b4(bA, sb, 0, 0);
+        auto sub = [&](half8_t (&bc)[4], half8_t (&bn)[4], const half8_t (&ac)[2], int i) {
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_setprio(1);
+            if (i < 7) read_b4(bn, sb, (i + 1) >> 2, (i + 1) & 3);
+            if (i == 3) {
+#pragma unroll
+                for (int f = 0; f < 2; ++f) a1[f] = dequant_frag<BITS>(w, 2 * f + 1, nz[f], sc[f]);
+            }
+#pragma unroll
+            for (int f = 0; f < 2; ++f)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    acc[f][4 * (i & 3) + r] =
+                        __builtin_amdgcn_mfma_f32_16x16x32_f16(ac[f], bc[r], acc[f][4 * (i & 3) + r], 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                if (j < 4) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+            }
+            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        sub(bA, bB, a0, 0);
+        sub(bB, bA, a0, 1);
+        sub(bA, bB, a0, 2);
+        sub(bB, bA, a0, 3);
+        sub(bA, bB, a1, 4);
+        sub(bB, bA, a1, 5);
+        sub(bA, bB, a1, 6);
+        sub(bB, bA, a1, 7);
+        if (issue) wait_prev();
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    stage(st0, 0);
+    if (nk > 1) stage(st1, 1);
+    if (nk > 1) wait_prev();
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    for (unsigned kt = 0; kt < nk; kt += 3) {
+        step(st0, st2, kt);
+        if (kt + 1 < nk) step(st1, st0, kt + 1);
+        if (kt + 2 < nk) step(st2, st1, kt + 2);
+    }
+
+    const bool vec_ok = (N % 4) == 0;
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+        const int nb0 = n0 + wave * 32 + 16 * f + 4 * (lane >> 4);
+        const float4 bv = *reinterpret_cast<const float4 *>(bias + nb0);
+        const bool full = (m0 + 256 <= M) && (nb0 + 4 <= N) && vec_ok;
+#pragma unroll
+        for (int r = 0; r < kRep; ++r) {
+            const int m = m0 + 16 * r + rl;
+            if constexpr (EPI == 1) {
+                if (m < M && nb0 < N)
+                    psample4(epi, m, nb0, N, acc[f][r][0] + bv.x, acc[f][r][1] + bv.y, acc[f][r][2] + bv.z,
+                             acc[f][r][3] + bv.w);
+            } else if (full) {
+                store4<YT>(Y + static_cast<size_t>(m) * N + nb0, acc[f][r][0] + bv.x, acc[f][r][1] + bv.y,
+                           acc[f][r][2] + bv.z, acc[f][r][3] + bv.w);
+            } else if (m < M) {
+                store_out4<YT>(Y + static_cast<size_t>(m) * N, bias, nb0, N, vec_ok, acc[f][r][0], acc[f][r][1],
+                               acc[f][r][2], acc[f][r][3]);
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Decode GEMM (small M, weight-streaming / HBM-bound): one block per 16-column n-tile
 // (N/16 blocks = 256 at N = 4096, one per CU), 8 waves split K by 128-deep slabs, 16x16x32
@@ -1338,6 +1542,13 @@ int launch_auto(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t
     const int np = static_cast<int>(h->Npad);
     const int mb256 = (M + 255) / 256, mb128 = (M + 127) / 128;
     if (np % 256 == 0 && mb256 * (np / 256) >= kCUs) {
+        if (h->variant == 8) {
+            const PSampleEpi ep = epi ? *epi : PSampleEpi{};
+            wq_gemm16_kernel<BITS, YT, EPI><<<static_cast<unsigned>(mb256 * (np / 256)), 512, 0, st>>>(
+                X, M, (int)h->K, h->w16, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, mb256, np / 256, ep);
+            DLLM_LAUNCH_CHECK();
+            return DLLM_OK;
+        }
         if (h->variant == 7) {
             const PSampleEpi ep = epi ? *epi : PSampleEpi{};
             wq_gemm_w2_kernel<BITS, YT, false, EPI><<<static_cast<unsigned>(mb256 * (np / 256)), 512, 0, st>>>(
@@ -1363,7 +1574,8 @@ int launch_auto(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t
 template <int BITS, typename YT>
 int launch_gemm_t(const dllm_linear *h, const __half *X, size_t M, YT *Y, hipStream_t st) {
     if (M <= static_cast<size_t>(kDecodeMaxM)) return launch_decode<BITS, YT>(h, X, M, Y, st);
-    if (h->variant == 4 || h->variant == 5 || h->variant == 7) return launch_auto<BITS, YT>(h, X, (int)M, Y, st);
+    if (h->variant == 4 || h->variant == 5 || h->variant == 7 || h->variant == 8)
+        return launch_auto<BITS, YT>(h, X, (int)M, Y, st);
     if (h->variant == 6) {   // previous policy: 2-stage kernels, 128-row tiles + split below 256 tiles
         const int tiles256 = static_cast<int>((M + kBM - 1) / kBM) * static_cast<int>(h->Npad / kBN);
         if (tiles256 < kCUs) return launch_mid<BITS, YT>(h, X, (int)M, Y, st);
@@ -1391,7 +1603,7 @@ int launch_gemm(const dllm_linear *h, const __half *X, size_t M, void *Y, int y_
 
 void free_linear(dllm_linear *h) {
     if (!h) return;
-    (void)hipFree(h->wdev); (void)hipFree(h->wdec); (void)hipFree(h->sz); (void)hipFree(h->canon); (void)hipFree(h->scales);
+    (void)hipFree(h->wdev); (void)hipFree(h->wdec); (void)hipFree(h->w16); (void)hipFree(h->sz); (void)hipFree(h->canon); (void)hipFree(h->scales);
     (void)hipFree(h->zps); (void)hipFree(h->bias); (void)hipFree(h->xws);
     delete h;
 }
@@ -1417,6 +1629,7 @@ int alloc_linear(size_t K, size_t N, uint8_t bits, size_t group, dllm_linear **o
     hipError_t e = hipSuccess;
     if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->wdev), h->Npad * K * bits / 8);
     if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->wdec), h->Npad * ((K + 127) / 128) * 128 * bits / 8);
+    if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->w16), h->Npad * K * bits / 8);
     if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->sz), h->G * h->Npad * 4);
     if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->canon), canon_words(K, N, bits) * 4);
     if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->scales), h->G * N * 4);
@@ -1435,6 +1648,8 @@ int finish_linear(dllm_linear *h, const float *bias, hipStream_t st) {
     if (bias) DLLM_HIP_TRY(hipMemcpyAsync(h->bias, bias, h->N * 4, hipMemcpyDeviceToDevice, st));
     dim3 gf(static_cast<unsigned>((h->Npad + 255) / 256), static_cast<unsigned>(h->K / 64));
     build_fragments_kernel<<<gf, 256, 0, st>>>(h->canon, h->K, h->N, h->Npad, h->bits, h->wdev);
+    DLLM_LAUNCH_CHECK();
+    build_fragments16_kernel<<<gf, 256, 0, st>>>(h->canon, h->K, h->N, h->Npad, h->bits, h->w16);
     DLLM_LAUNCH_CHECK();
     dim3 gd(static_cast<unsigned>((h->Npad + 255) / 256), static_cast<unsigned>((h->K + 127) / 128));
     build_decode_kernel<<<gd, 256, 0, st>>>(h->canon, h->K, h->N, h->Npad, h->bits, h->wdec);
@@ -1552,7 +1767,8 @@ int dllm_linear_forward_psample(dllm_linear_t h, const void *X, size_t M, int x_
     hipStream_t st = as_stream(stream);
     const __half *Xh = nullptr;
     if (const int rc = prepare_x(h, X, M, x_dtype, st, &Xh)) return rc;
-    if (M <= static_cast<size_t>(kDecodeMaxM) || (h->variant != 4 && h->variant != 5 && h->variant != 7)) {
+    if (M <= static_cast<size_t>(kDecodeMaxM) ||
+        (h->variant != 4 && h->variant != 5 && h->variant != 7 && h->variant != 8)) {
         // Paths without the fused epilogue: f32 eps through a per-stream workspace, then p_sample
         // (the same eps bits, hence the same result as the fused form on that path).
         float *eps = device_workspace(st, M * h->N * sizeof(float), 1);
@@ -1618,7 +1834,7 @@ int dllm_linear_set_kernel_variant(dllm_linear_t h, int variant) {
         h->rlab = variant - 32;
         return DLLM_OK;
     }
-    if (variant < 0 || variant > 7) return fail(DLLM_ERR_INVALID_PARAMS, "variant must be 0..7 (16..23, 32..47: ablations)");
+    if (variant < 0 || variant > 8) return fail(DLLM_ERR_INVALID_PARAMS, "variant must be 0..8 (16..23, 32..95: ablations)");
     h->variant = variant;
     h->dlab = h->rlab = 0;
     return DLLM_OK;

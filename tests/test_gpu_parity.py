@@ -273,6 +273,10 @@ def test_linear_full_size_vs_torch_fp32(dllm, torch, orc):
     Yr = X.float() @ Wh
     rel = (torch.linalg.norm(Y - Yr) / torch.linalg.norm(Yr)).item()
     assert rel <= REL_TOL, rel
+    lin.set_kernel_variant(8)   # the 16x16x32 MFMA kernel
+    Y8 = lin(X, out_dtype=torch.float16).float()
+    rel = (torch.linalg.norm(Y8 - Yr) / torch.linalg.norm(Yr)).item()
+    assert rel <= REL_TOL, ("variant 8", rel)
 
 
 @pytest.mark.parametrize("M", [65, 256, 512, 1024, 1500, 2048])
@@ -315,6 +319,26 @@ def test_linear_split_k_exact_integers(dllm, torch, orc):
     lin = dllm.QuantLinear.from_weight(dev(torch, W), None, 4, 128)
     Y = host(lin(dev(torch, X).half(), out_dtype=torch.float32))
     assert np.array_equal(Y, (X.astype(np.float64) @ W.astype(np.float64)).astype(np.float32))
+
+
+@pytest.mark.parametrize("variant", [4, 8])
+@pytest.mark.parametrize("bits", [2, 4, 8])
+def test_linear_big_tile_exact_integers(dllm, torch, orc, variant, bits):
+    """256x256-tile kernels (variant 4: 32x32x16 MFMA, w-layout; variant 8: 16x16x32 MFMA, w16
+    layout) on exact-integer data at M = N = 4096 (K = 256, so the f16 products and f32 sums are
+    exact): the result must equal the f64 product bit for bit, catching any fragment-map error."""
+    K, N, M = 256, 4096, 4096
+    rng = np.random.default_rng(31 + bits)
+    q = (1 << bits) - 1
+    W = rng.integers(0, q + 1, (K, N)).astype(np.float32)
+    for g0 in range(0, K, 128):
+        W[g0, :], W[g0 + 1, :] = 0.0, float(q)
+    X = rng.integers(-2, 3, (M, K)).astype(np.float32)
+    lin = dllm.QuantLinear.from_weight(dev(torch, W), None, bits, 128)
+    lin.set_kernel_variant(variant)
+    Y = host(lin(dev(torch, X).half(), out_dtype=torch.float32))
+    assert np.array_equal(Y, (X.astype(np.float64) @ W.astype(np.float64)).astype(np.float32))
+    lin.close()
 
 
 def test_mixed_precision_stack(dllm, torch, orc):
