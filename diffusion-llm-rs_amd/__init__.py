@@ -20,12 +20,13 @@ from . import _lib
 from ._lib import (CalibrationRequired, HipError, InvalidParams, QuantizationError, SerializationError,
                    ShapeMismatch, UnsupportedOperation)
 from . import quantization, quant, kvquant, linear, parallel, diffusion, serde
-from .quantization import (QuantizedKVCacheEntry, QuantizedTensor, compression_ratio, dequantize_tensor, kv_attention,
+from .quantization import (AdaptiveQuantizer, QuantizedKVCacheEntry, QuantizedTensor, compression_ratio, dequantize_tensor, kv_attention,
                            pack, quantize_tensor, unpack)
 from .quant import CalibrationData, DefaultQuantizer, QuantizationParams, QuantizationType, quant_utils
 from .kvquant import BitQuantizer, PrefillKVQuant, SystemConfig, compress_vectors, decompress_vectors
 from .linear import MixedPrecisionStack, QuantLinear
-from .diffusion import (AlphaMode, BetaSchedule, Cumprod, DenoiseLoop, DiffusionConfig, KVCacheEntry, add_noise,
+from .diffusion import (AlphaMode, BetaSchedule, Cumprod, DenoiseLoop, DiffusionConfig, KVCacheEntry, KVCacheStore,
+                        add_noise,
                         p_sample, randn)
 
 __all__ = [
@@ -34,7 +35,7 @@ __all__ = [
     "CalibrationData", "BitQuantizer", "PrefillKVQuant", "SystemConfig", "compress_vectors", "decompress_vectors",
     "QuantLinear", "MixedPrecisionStack", "QuantizationError", "InvalidParams", "UnsupportedOperation",
     "ShapeMismatch", "CalibrationRequired", "HipError", "BetaSchedule", "Cumprod", "AlphaMode", "DiffusionConfig",
-    "KVCacheEntry", "DenoiseLoop", "add_noise", "p_sample", "randn",
+    "KVCacheEntry", "KVCacheStore", "DenoiseLoop", "add_noise", "p_sample", "randn", "AdaptiveQuantizer",
 ]
 
 

@@ -88,6 +88,9 @@ SIGNATURES = {
     "dllm_default_dequantize": (INT, [P, S, FL, I32, P, P]),
     "dllm_calib_update": (INT, [P, S, P, P, S, P, S, P]),
     "dllm_calib_compute_params": (INT, [FL, FL, S, U8, INT, P, P]),
+    "dllm_adaptive_update": (INT, [P, S, P, P, S, P]),
+    "dllm_adaptive_compute_params": (INT, [P, INT, U32, P, P]),
+    "dllm_adaptive_quantize": (INT, [P, S, U32, P, INT, P, P]),
     "dllm_bit_quantize": (INT, [P, S, U32, FL, FL, P, P]),
     "dllm_bit_dequantize": (INT, [P, S, FL, FL, P, INT, P]),
     "dllm_quantize_vectors": (INT, [P, S, S, P, S, P, S, P, P, P]),

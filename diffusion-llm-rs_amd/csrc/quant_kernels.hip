@@ -402,10 +402,12 @@ __global__ void __launch_bounds__(kBlock) decompress_rows_kernel(const uint8_t *
 // ---------------------------------------------------------------------------------------------
 // a10: CalibrationData::update (quantization/src/calibrate.rs:42-69) on the device.
 // ---------------------------------------------------------------------------------------------
+// seed: the fold's start value, f32::MAX for calibrate.rs:43 (MIN/MAX seeds), +inf for the
+// adaptive quantizer's exact extremes.
 __global__ void __launch_bounds__(kBlock) calib_fold_kernel(const float2 *__restrict__ partials, int np,
-                                                            float *__restrict__ stats) {
+                                                            float *__restrict__ stats, float seed) {
     __shared__ float smem[2 * kBlock / 64];
-    float mx = -3.40282347e+38f, mn = 3.40282347e+38f;   // fold seeds (f32::MIN, f32::MAX), :43
+    float mx = -seed, mn = seed;
     for (int i = threadIdx.x; i < np; i += kBlock) { float2 p = partials[i]; mx = fmaxf(mx, p.x); mn = fminf(mn, p.y); }
     block_minmax(mx, mn, smem);
     if (threadIdx.x == 0) {
@@ -442,6 +444,52 @@ __global__ void __launch_bounds__(kBlock) calib_hist_kernel(const float *__restr
         __syncthreads();
         for (int b = threadIdx.x; b < num_bins; b += kBlock)
             if (lhist[b]) atomicAdd(&hist[b], static_cast<unsigned long long>(lhist[b]));
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// 8f rank 4: AdaptiveQuantizer (diffuse-llm-rs/src/quantization.rs:178-235).
+// ---------------------------------------------------------------------------------------------
+// compute_params (:206-217): query(0.0/1.0).unwrap_or(0.0/1.0); scale without a zero guard;
+// zp = round(-min / scale).clamp(0, q_max) -- round first, NaN passes the clamp.
+__global__ void adaptive_params_kernel(const float *__restrict__ stats, int has_samples, uint32_t bits,
+                                       float *__restrict__ params) {
+    if (threadIdx.x != 0) return;
+    const float mn = has_samples ? stats[0] : 0.0f;
+    const float mx = has_samples ? stats[1] : 1.0f;
+    const float q_max = static_cast<float>(1u << bits) - 1.0f;  // :212
+    const float scale = (mx - mn) / q_max;                        // :213
+    const float m = -mn;
+    params[0] = scale;
+    params[1] = rs_clamp(roundf(m / scale), 0.0f, q_max);         // :214
+}
+
+// quantize (:220-234), one code per byte: (round(x/scale + zp) as i32).clamp(0, hi) as u8, where
+// hi = q_max as i32 and `as u8` keeps the low byte (bits > 8).  Four elements per thread.
+__global__ void __launch_bounds__(kBlock) adaptive_quantize_kernel(const float *__restrict__ x, size_t n, int hi,
+                                                                   const float *__restrict__ params,
+                                                                   uint8_t *__restrict__ out) {
+    const float scale = params[0], zp = params[1];
+    const size_t nq = (n + 3) / 4;
+    for (size_t o = blockIdx.x * static_cast<size_t>(kBlock) + threadIdx.x; o < nq;
+         o += static_cast<size_t>(gridDim.x) * kBlock) {
+        const size_t i0 = 4 * o;
+        uint32_t word = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (i0 + j < n) {
+                float t = x[i0 + j] / scale;
+                t = t + zp;
+                word |= (rs_round_i32_clamp(t, hi) & 0xffu) << (8 * j);
+            }
+        }
+        if (i0 + 4 <= n) {
+            if ((reinterpret_cast<uintptr_t>(out + i0) & 3) == 0) {
+                *reinterpret_cast<uint32_t *>(out + i0) = word;
+                continue;
+            }
+        }
+        for (int j = 0; j < 4 && i0 + j < n; ++j) out[i0 + j] = static_cast<uint8_t>(word >> (8 * j));
     }
 }
 
@@ -581,7 +629,7 @@ int dllm_calib_update(const float *x, size_t n, float *stats, uint64_t *histogra
     float2 *partials = static_cast<float2 *>(workspace);
     int rc = launch_minmax(x, n, partials, nblk, st);
     if (rc) return rc;
-    calib_fold_kernel<<<1, kBlock, 0, st>>>(partials, static_cast<int>(nblk), stats);
+    calib_fold_kernel<<<1, kBlock, 0, st>>>(partials, static_cast<int>(nblk), stats, 3.40282347e+38f);
     DLLM_LAUNCH_CHECK();
     if (num_bins && histogram) {
         if (num_bins > 0x7fffffff) return fail(DLLM_ERR_INVALID_PARAMS, "num_bins too large");
@@ -590,6 +638,51 @@ int dllm_calib_update(const float *x, size_t n, float *stats, uint64_t *histogra
             x, n, stats, reinterpret_cast<unsigned long long *>(histogram), static_cast<int>(num_bins), use_lds);
         DLLM_LAUNCH_CHECK();
     }
+    return DLLM_OK;
+}
+
+int dllm_adaptive_update(const float *x, size_t n, float *stats, void *workspace, size_t workspace_bytes,
+                         dllm_stream_t stream) {
+    if (!stats || (n && !x)) return fail(DLLM_ERR_INVALID_PARAMS, "null pointer");
+    if (!n) return DLLM_OK;
+    const unsigned nblk = minmax_blocks(n);
+    if (!workspace || workspace_bytes < sizeof(float2) * nblk)
+        return fail(DLLM_ERR_INVALID_PARAMS, "workspace too small (see dllm_quantize_tensor_workspace)");
+    hipStream_t st = as_stream(stream);
+    float2 *partials = static_cast<float2 *>(workspace);
+    int rc = launch_minmax(x, n, partials, nblk, st);
+    if (rc) return rc;
+    calib_fold_kernel<<<1, kBlock, 0, st>>>(partials, static_cast<int>(nblk), stats, INFINITY);
+    DLLM_LAUNCH_CHECK();
+    return DLLM_OK;
+}
+
+int dllm_adaptive_compute_params(const float *stats, int has_samples, uint32_t bits, float *params,
+                                 dllm_stream_t stream) {
+    if (bits > 31) return fail(DLLM_ERR_INVALID_PARAMS, "1u32 << bits overflows");
+    if (!params || (has_samples && !stats)) return fail(DLLM_ERR_INVALID_PARAMS, "null pointer");
+    adaptive_params_kernel<<<1, 64, 0, as_stream(stream)>>>(stats, has_samples ? 1 : 0, bits, params);
+    DLLM_LAUNCH_CHECK();
+    return DLLM_OK;
+}
+
+int dllm_adaptive_quantize(const float *x, size_t n, uint32_t bits, const float *params, int packed, uint8_t *out,
+                           dllm_stream_t stream) {
+    if (bits > 31) return fail(DLLM_ERR_INVALID_PARAMS, "1u32 << bits overflows");
+    if (packed && (bits < 1 || bits > 8)) return fail(DLLM_ERR_INVALID_PARAMS, "packed output needs 1 <= bits <= 8");
+    if (!params || (n && (!x || !out))) return fail(DLLM_ERR_INVALID_PARAMS, "null pointer");
+    if (!n) return DLLM_OK;
+    hipStream_t st = as_stream(stream);
+    if (bits >= 1 && bits <= 8) {
+        // Same map as quantize_tensor (quantization.rs:61-64 == :225-230), hi = 2^bits - 1.
+        quantize_tensor_kernel<<<octet_grid(n), kBlock, 0, st>>>(x, n, bits, packed, out, params, aligned(x, 16),
+                                                                 aligned(out, 8));
+    } else {
+        const float qf = static_cast<float>(1u << bits) - 1.0f;
+        const int hi = qf >= 2147483648.0f ? INT32_MAX : static_cast<int>(qf);   // `q_max as i32`
+        adaptive_quantize_kernel<<<grid_for((n + 3) / 4, kBlock, kCUs * 16), kBlock, 0, st>>>(x, n, hi, params, out);
+    }
+    DLLM_LAUNCH_CHECK();
     return DLLM_OK;
 }
 

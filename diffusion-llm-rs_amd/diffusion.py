@@ -216,6 +216,15 @@ class KVCacheEntry:
         if self.decode_quant_bits > 0:
             self.decode_quantized = QuantizedKVCacheEntry.new(new_keys, new_values, self.decode_quant_bits)
 
+    def clone(self) -> "KVCacheEntry":
+        """``#[derive(Clone)]``: an independent copy (device tensors duplicated)."""
+        c = object.__new__(KVCacheEntry)
+        c.__dict__.update(self.__dict__)
+        c.keys, c.values = self.keys.clone(), self.values.clone()
+        c.prefill_quantized = None if self.prefill_quantized is None else self.prefill_quantized.clone()
+        c.decode_quantized = None if self.decode_quantized is None else self.decode_quantized.clone()
+        return c
+
     def memory_usage(self) -> int:
         """lib.rs:279-302: packed bytes of the quantized copies, else f32 bytes."""
         total = sum(q.memory_usage() for q in (self.prefill_quantized, self.decode_quantized) if q is not None)
@@ -226,6 +235,105 @@ class KVCacheEntry:
 
     def is_empty(self) -> bool:
         return self.seq_len == 0
+
+
+_USIZE = 1 << 64
+
+
+class KVCacheStore:
+    """DiffuseLLM's KV-cache registry: ``kv_cache: DashMap<String, KVCacheEntry>`` and
+    ``cache_memory_usage: AtomicUsize`` (lib.rs:338-345) with
+    ``init_kv_cache`` (:958-980), ``get_or_init_cache`` (:983-991), ``update_kv_cache`` (:994-1043),
+    ``evict_oldest_entries`` (:1046-1073), ``clear_kv_cache`` (:1076-1079) and
+    ``kv_cache_memory_usage`` (:1082-1084).
+
+    The accounting is the reference's, quirks included:
+    - The eviction check prices an update at ``keys.len() * 4 * 2`` bytes, f32 K + V.
+    - A new entry adds its packed ``memory_usage()``.
+    - An update of an existing entry adds ``new_size.saturating_sub(old_size)``.
+    - Eviction removes the LARGEST entries first, despite its name, until the freed bytes reach the
+      request. It then subtracts them with the wrapping ``fetch_sub`` of an AtomicUsize.
+    - ``get_or_init_cache`` inserts a fresh entry without accounting, and hands out a clone.
+    Ties in the size order keep insertion order; the DashMap's iteration order is unspecified.
+    The entries' K/V and quantized copies live on the device; evicting an entry frees them. The
+    reference's update path calls ``KVCacheEntry::new`` with one width (:1028-1032), so a new entry
+    there uses ``kv_quant_bits`` for both phases."""
+
+    def __init__(self, config: DiffusionConfig, entry_factory: Optional[Callable] = None, device="cuda"):
+        self.config = config
+        self.entry_factory = entry_factory or KVCacheEntry.new
+        self.device = device
+        self.kv_cache: dict = {}
+        self.cache_memory_usage = 0
+        self._lock = __import__("threading").RLock()
+
+    def _phase_bits(self):
+        c = self.config
+        return (c.prefill_bits, c.decode_bits) if c.use_phase_aware_quant else (c.kv_quant_bits, c.kv_quant_bits)
+
+    def init_kv_cache(self, batch_size: int):
+        """:958-980 -- empty [num_layers, 0, heads * head_dim] K/V at the phase widths."""
+        c = self.config
+        hd = (c.hidden_size // c.num_attention_heads) * c.num_attention_heads
+        z = torch.zeros((c.num_layers, 0, hd), dtype=torch.float32, device=self.device)
+        pb, db = self._phase_bits()
+        return self.entry_factory(z, z.clone(), pb, db)
+
+    def get_or_init_cache(self, cache_id: str, batch_size: int):
+        """:983-991 -- a clone of the stored entry; a missing one is created and inserted."""
+        with self._lock:
+            e = self.kv_cache.get(cache_id)
+            if e is None:
+                e = self.init_kv_cache(batch_size)
+                self.kv_cache[cache_id] = e
+            return e.clone()
+
+    def update_kv_cache(self, cache_id: str, keys: torch.Tensor, values: torch.Tensor) -> None:
+        """:994-1043."""
+        c = self.config
+        if not c.use_kv_cache:
+            return
+        with self._lock:
+            entry_size = keys.numel() * 4 * 2
+            new_usage = self.cache_memory_usage + entry_size
+            if new_usage > c.max_cache_size:
+                self.evict_oldest_entries(new_usage - c.max_cache_size)
+            e = self.kv_cache.get(cache_id)
+            if e is not None:
+                old_size = e.memory_usage()
+                new_size = keys.numel() * 4 * 2
+                e.update(keys, values)
+                self.cache_memory_usage = (self.cache_memory_usage + max(new_size - old_size, 0)) % _USIZE
+            else:
+                e = self.entry_factory(keys, values, c.kv_quant_bits, c.kv_quant_bits)
+                self.kv_cache[cache_id] = e
+                self.cache_memory_usage = (self.cache_memory_usage + e.memory_usage()) % _USIZE
+
+    def evict_oldest_entries(self, bytes_to_free: int) -> None:
+        """:1046-1073 -- largest entries first until ``bytes_to_free`` is reached."""
+        with self._lock:
+            entries = sorted(((k, v.memory_usage()) for k, v in self.kv_cache.items()), key=lambda kv: -kv[1])
+            freed = 0
+            for key, size in entries:
+                if freed >= bytes_to_free:
+                    break
+                if self.kv_cache.pop(key, None) is not None:
+                    freed += size
+            self.cache_memory_usage = (self.cache_memory_usage - freed) % _USIZE
+
+    def clear_kv_cache(self) -> None:
+        with self._lock:
+            self.kv_cache.clear()
+            self.cache_memory_usage = 0
+
+    def kv_cache_memory_usage(self) -> int:
+        return self.cache_memory_usage
+
+    def __contains__(self, cache_id):
+        return cache_id in self.kv_cache
+
+    def __len__(self):
+        return len(self.kv_cache)
 
 
 def progressive_bits(config: DiffusionConfig, num_steps: int, t: int) -> int:
@@ -304,7 +412,7 @@ class DenoiseLoop:
             return None
         is_prefill = t > num_steps // 2
         c.set_phase(is_prefill)
-        if self.config.progressive_precision and not is_prefill:
+        if self.config.use_phase_aware_quant and self.config.progressive_precision and not is_prefill:
             tb = progressive_bits(self.config, num_steps, t)
             if tb != c.decode_quant_bits:
                 c.decode_quant_bits = tb
@@ -314,7 +422,24 @@ class DenoiseLoop:
         c.update(keys, values)
         return k, v
 
-    def sample(self, x: torch.Tensor, num_steps: Optional[int] = None) -> torch.Tensor:
+    def sample(self, x: torch.Tensor, num_steps: Optional[int] = None, store: Optional[KVCacheStore] = None,
+               cache_id: Optional[str] = None) -> torch.Tensor:
+        """The loop of lib.rs:880-931.  With a ``store`` and ``cache_id`` (and use_kv_cache) the
+        cache is the reference's: a clone of the stored entry (get_or_init_cache, prefill phase,
+        :864-872), saved back at the end as its dequantized K/V (update_kv_cache, :936-943)."""
+        if store is not None and cache_id is not None and self.config.use_kv_cache:
+            kv = store.get_or_init_cache(cache_id, 1)
+            kv.set_phase(True)
+            saved, self.kv_cache = self.kv_cache, kv
+            try:
+                x = self._sample(x, num_steps)
+            finally:
+                self.kv_cache = saved
+            store.update_kv_cache(cache_id, kv.get_keys(), kv.get_values())
+            return x
+        return self._sample(x, num_steps)
+
+    def _sample(self, x: torch.Tensor, num_steps: Optional[int] = None) -> torch.Tensor:
         num_steps = num_steps or self.config.num_timesteps
         x = x.to(device="cuda", dtype=torch.float32).contiguous()
         buf = torch.empty_like(x)

@@ -8,6 +8,7 @@ on the device as a 2-float tensor until read, so nothing synchronises the stream
 from __future__ import annotations
 
 import math
+import threading
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -154,6 +155,9 @@ class QuantizedTensor:
         """quantization.rs:120-124: ``(prod(shape) * 4) / ceil(len * bits / 8)``."""
         return compression_ratio(self.numel(), self.numel(), self.bits)
 
+    def clone(self) -> "QuantizedTensor":
+        return QuantizedTensor(self.data.clone(), self.shape, self.params.clone(), self.bits, self.packed)
+
 
 @dataclass
 class QuantizedKVCacheEntry:
@@ -178,6 +182,9 @@ class QuantizedKVCacheEntry:
         """quantization.rs:169-175."""
         return self.values.dequantize(out_dtype).reshape(self.values.shape)
 
+    def clone(self) -> "QuantizedKVCacheEntry":
+        return QuantizedKVCacheEntry(self.keys.clone(), self.values.clone(), self.seq_len)
+
     def memory_usage(self) -> int:
         """Packed bytes of K and V (the accounting of diffuse-llm-rs/src/lib.rs:279-302)."""
         return sum(packed_bytes(t.numel(), t.bits) for t in (self.keys, self.values))
@@ -200,3 +207,56 @@ def kv_attention(q: torch.Tensor, keys: QuantizedTensor, values: QuantizedTensor
     check(_lib.load().dllm_kv_attention(_ptr(qd), _ptr(keys.data), _ptr(keys.params), _ptr(values.data),
                                         _ptr(values.params), keys.bits, S, H, D, _ptr(out), _stream()))
     return out
+
+
+class AdaptiveQuantizer:
+    """``AdaptiveQuantizer`` (quantization.rs:178-235): bits, target_ratio, and running statistics
+    behind a lock (the reference's ``Arc<Mutex<CKMS<f32>>>``).
+
+    The statistics stay on the device as {min, max} (dllm_adaptive_update).  The reference queries
+    its CKMS(0.01) summary only at q = 0.0 and q = 1.0 (:209-210); the exact extremes answer those
+    queries with rank error 0, inside CKMS's eps*n bound.  NaN samples are skipped.  Parity is
+    unpinned: the quantiles crate is absent.  ``target_ratio`` is stored and unused, as in the
+    reference."""
+
+    def __init__(self, bits: int, target_ratio: float, device="cuda"):
+        self.bits, self.target_ratio = int(bits), float(target_ratio)
+        self._lock = threading.Lock()
+        self._stats = torch.tensor([math.inf, -math.inf], dtype=torch.float32, device=device)
+        self._count = 0
+
+    def update_stats(self, data) -> None:
+        """:198-203 -- every element inserted into the summary."""
+        x = _dev(data, torch.float32).reshape(-1)
+        n = x.numel()
+        if n == 0:
+            return
+        L = _lib.load()
+        ws = torch.empty(max(L.dllm_quantize_tensor_workspace(n), 16), dtype=torch.uint8, device=x.device)
+        with self._lock:
+            check(L.dllm_adaptive_update(_ptr(x), n, _ptr(self._stats), _ptr(ws), ws.numel(), _stream()))
+            self._count += n
+
+    def compute_params_device(self) -> torch.Tensor:
+        """:206-217 as a device f32[2] {scale, zero_point}; nothing synchronises the stream."""
+        params = torch.empty(2, dtype=torch.float32, device=self._stats.device)
+        with self._lock:
+            check(_lib.load().dllm_adaptive_compute_params(_ptr(self._stats), int(self._count > 0), self.bits,
+                                                           _ptr(params), _stream()))
+        return params
+
+    def compute_params(self) -> tuple[float, float]:
+        """:206-217 ``-> (f32, f32)`` (reads the two floats back)."""
+        s, z = self.compute_params_device().cpu().tolist()
+        return s, z
+
+    def quantize(self, data, packed: bool = False):
+        """:220-234 ``-> (Vec<u8>, f32, f32)``: codes u8 (one per element, or the packed stream for
+        1 <= bits <= 8) and the device params {scale, zero_point} used."""
+        x = _dev(data, torch.float32).reshape(-1)
+        n = x.numel()
+        params = self.compute_params_device()
+        out = torch.empty(packed_bytes(n, self.bits) if packed else n, dtype=torch.uint8, device=x.device)
+        check(_lib.load().dllm_adaptive_quantize(_ptr(x) if n else None, n, self.bits, _ptr(params), int(packed),
+                                                 _ptr(out) if out.numel() else None, _stream()))
+        return out, params

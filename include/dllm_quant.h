@@ -109,6 +109,25 @@ int dllm_calib_update(const float *x, size_t n, float *stats, uint64_t *histogra
 int dllm_calib_compute_params(float min, float max, size_t total_samples, uint8_t bits, int symmetric,
                               float *scale, int32_t *zero_point);
 
+/* ---- 8f rank 4: AdaptiveQuantizer (diffuse-llm-rs/src/quantization.rs:178-235) -------------
+ * Replaces AdaptiveQuantizer::{update_stats, compute_params, quantize} (:198-234).
+ * stats[2] DEVICE {min, max}, initialised by the caller to {+inf, -inf}.  The reference's
+ * statistics are a quantiles-0.7 CKMS<f32>(0.01) queried only at q = 0.0 and q = 1.0 (:209-210);
+ * update folds x into the exact extremes instead (rank error 0, inside CKMS's eps*n bound; NaN
+ * skipped; parity unpinned: the crate is absent).  Workspace: dllm_quantize_tensor_workspace(n).
+ * compute_params writes params[2] = {scale, zero_point} on the device:
+ *   min, max = stats, or the unwrap_or defaults 0.0 / 1.0 when has_samples == 0;
+ *   scale = (max - min) / (2^bits - 1) (no zero guard); zp = round(-min / scale).clamp(0, q_max).
+ * quantize: q = (round(x / scale + zp) as i32).clamp(0, q_max as i32) as u8 (the low byte when
+ * bits > 8).  packed = 1 needs 1 <= bits <= 8; unpacked accepts 0..=31; bits > 31 -> INVALID_PARAMS
+ * (1u32 << bits overflows). */
+int dllm_adaptive_update(const float *x, size_t n, float *stats, void *workspace, size_t workspace_bytes,
+                         dllm_stream_t stream);
+int dllm_adaptive_compute_params(const float *stats, int has_samples, uint32_t bits, float *params,
+                                 dllm_stream_t stream);
+int dllm_adaptive_quantize(const float *x, size_t n, uint32_t bits, const float *params, int packed, uint8_t *out,
+                           dllm_stream_t stream);
+
 /* ---- a8-ii: prefill-kvquant-rs kvquant::BitQuantizer (prefill-kvquant-rs/lib.rs:29-53) ------
  * quantize: q = ((x - zp) / scale).clamp(0, (1<<bits)-1) as u8  (truncation, no rounding);
  * dequantize: y = q as f32 * scale + zp.  bits > 30 -> INVALID_PARAMS (i32 shift overflow). */

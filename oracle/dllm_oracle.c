@@ -272,6 +272,43 @@ int orc_calib_compute_params(const orc_calib_t *c, uint8_t bits, int symmetric, 
     return ORC_OK;
 }
 
+/* ---- 8f rank 4: AdaptiveQuantizer (diffuse-llm-rs/src/quantization.rs:178-235) ----------- */
+/* The statistics are a quantiles-0.7 CKMS<f32>(0.01) (third-party, absent) queried only at
+ * q = 0.0 and q = 1.0 (:209-210).  Restated as the exact extremes of the inserted samples: rank
+ * error 0, inside CKMS's eps*n guarantee; NaN samples are skipped.  Parity unpinned beyond the
+ * reference's property test (:267-277). */
+void orc_adaptive_update(float *minmax, const float *x, size_t n) {
+    for (size_t i = 0; i < n; ++i) { minmax[0] = fminf(minmax[0], x[i]); minmax[1] = fmaxf(minmax[1], x[i]); }
+}
+
+/* :206-217 compute_params: query(..).unwrap_or(0.0 / 1.0) when no sample was inserted;
+ * scale = (max - min) / q_max (no zero guard); zp = round(-min / scale).clamp(0, q_max)
+ * (round, THEN clamp; NaN passes). */
+int orc_adaptive_params(const float *minmax, int has_samples, uint32_t bits, float *scale, float *zero_point) {
+    if (bits > 31) return ORC_INVALID_PARAMS;          /* 1u32 << bits overflows -> panic */
+    const float mn = has_samples ? minmax[0] : 0.0f;
+    const float mx = has_samples ? minmax[1] : 1.0f;
+    const float q_max = (float)(1u << bits) - 1.0f;     /* :212 */
+    const float s = (mx - mn) / q_max;                  /* :213 */
+    const float m = -mn;
+    *scale = s;
+    *zero_point = rs_clamp(roundf(m / s), 0.0f, q_max); /* :214 */
+    return ORC_OK;
+}
+
+/* :220-234 quantize: ((x / scale) + zp).round() as i32, .clamp(0, q_max as i32) as u8 -- the
+ * `as u8` of an i32 keeps the low byte, which matters only for bits > 8. */
+int orc_adaptive_quantize(const float *x, size_t n, uint32_t bits, float scale, float zero_point, uint8_t *out) {
+    if (bits > 31) return ORC_INVALID_PARAMS;
+    const int32_t hi = rs_as_i32((float)(1u << bits) - 1.0f);
+    for (size_t i = 0; i < n; ++i) {
+        const float t = x[i] / scale;
+        const float u = t + zero_point;
+        out[i] = (uint8_t)(rs_clamp_i32(rs_as_i32(roundf(u)), 0, hi) & 0xff);
+    }
+    return ORC_OK;
+}
+
 /* ---- a5: group-wise composition + linear layer ----------------------------------------- */
 
 int orc_quantize_weights(const float *W, size_t K, size_t N, uint8_t bits, size_t group,

@@ -80,6 +80,12 @@ void orc_calib_init(orc_calib_t *c, size_t num_bins, uint64_t *hist_storage);
 void orc_calib_update(orc_calib_t *c, const float *x, size_t n);
 int orc_calib_compute_params(const orc_calib_t *c, uint8_t bits, int symmetric, float *scale, int32_t *zero_point);
 
+/* 8f rank 4: diffuse-llm-rs/src/quantization.rs:178-235 AdaptiveQuantizer (CKMS q = 0 / 1 as
+ * exact extremes; minmax = {min, max}, start {+inf, -inf}). */
+void orc_adaptive_update(float *minmax, const float *x, size_t n);
+int orc_adaptive_params(const float *minmax, int has_samples, uint32_t bits, float *scale, float *zero_point);
+int orc_adaptive_quantize(const float *x, size_t n, uint32_t bits, float scale, float zero_point, uint8_t *out);
+
 /* a5 (build-defined composition): per (column n, K-group g) a1 with `bits`, then a2.
  *   W [K][N] f32 row-major (reference layout, diffuse-llm-rs/src/lib.rs:776-777).
  *   codes [K][N] u8, scales [G][N] f32, zps [G][N] u8, G = ceil(K/group). */

@@ -57,6 +57,9 @@ def lib():
             "orc_randn": (None, [C.c_uint64, C.c_uint64, S, P]),
             "orc_p_sample": (None, [P, P, P, P, S, S, C.c_int, P]),
             "orc_add_noise": (None, [P, P, P, S, S, P]),
+            "orc_adaptive_update": (None, [P, P, S]),
+            "orc_adaptive_params": (C.c_int, [P, C.c_int, C.c_uint32, P, P]),
+            "orc_adaptive_quantize": (C.c_int, [P, S, C.c_uint32, F, F, P]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -261,3 +264,31 @@ def add_noise(x0, noise, coef):
     lib().orc_add_noise(_p(x0), _p(np.ascontiguousarray(noise, np.float32)),
                         _p(np.ascontiguousarray(coef, np.float32)), B, D, _p(out))
     return out
+
+
+# ---- 8f rank 4: AdaptiveQuantizer (diffuse-llm-rs/src/quantization.rs:178-235) ---------------
+
+class AdaptiveQuantizer:
+    """Oracle mirror of the reference's AdaptiveQuantizer (CKMS q = 0 / 1 as exact extremes)."""
+
+    def __init__(self, bits: int, target_ratio: float = 4.0):
+        self.bits, self.target_ratio = bits, target_ratio
+        self.minmax = np.array([np.inf, -np.inf], np.float32)
+        self.count = 0
+
+    def update_stats(self, data):
+        x = np.ascontiguousarray(data, np.float32).ravel()
+        lib().orc_adaptive_update(_p(self.minmax), _p(x), x.size)
+        self.count += x.size
+
+    def compute_params(self):
+        s, z = C.c_float(), C.c_float()
+        _check(lib().orc_adaptive_params(_p(self.minmax), int(self.count > 0), self.bits, C.byref(s), C.byref(z)))
+        return np.float32(s.value), np.float32(z.value)
+
+    def quantize(self, data):
+        x = np.ascontiguousarray(data, np.float32).ravel()
+        s, z = self.compute_params()
+        out = np.zeros(x.size, np.uint8)
+        _check(lib().orc_adaptive_quantize(_p(x), x.size, self.bits, float(s), float(z), _p(out)))
+        return out, s, z

@@ -225,6 +225,39 @@ class Calibration:
         return scale, zp
 
 
+# ---- 8f rank 4: AdaptiveQuantizer (diffuse-llm-rs/src/quantization.rs:178-235) --------------
+
+class AdaptiveQuantizer:
+    """quantization.rs:178-235; the CKMS q = 0.0 / 1.0 queries (:209-210) as exact extremes."""
+
+    def __init__(self, bits: int, target_ratio: float = 4.0):
+        self.bits, self.target_ratio = bits, target_ratio
+        self.min, self.max, self.count = F32(np.inf), F32(-np.inf), 0
+
+    def update_stats(self, data):
+        x = np.asarray(data, F32).ravel()
+        self.min = F32(np.fmin(self.min, fold_min(x)))
+        self.max = F32(np.fmax(self.max, fold_max(x)))
+        self.count += x.size
+
+    def compute_params(self):
+        mn, mx = (self.min, self.max) if self.count else (F32(0.0), F32(1.0))
+        q_max = F32(F32(2.0 ** self.bits) - F32(1.0))
+        with np.errstate(divide="ignore", invalid="ignore"):
+            scale = F32(F32(mx - mn) / q_max)
+            zp = rs_clamp(rs_round(np.array([F32(-mn) / scale], F32)), 0.0, q_max)[0]
+        return scale, F32(zp)
+
+    def quantize(self, data):
+        x = np.asarray(data, F32).ravel()
+        scale, zp = self.compute_params()
+        hi = int(rs_as_i32(np.array([F32(2.0 ** self.bits) - F32(1.0)], F32))[0])
+        with np.errstate(divide="ignore", invalid="ignore"):
+            t = ((x / scale).astype(F32) + zp).astype(F32)
+        q = np.clip(rs_as_i32(rs_round(t)), 0, hi)
+        return (q & 0xFF).astype(np.uint8), scale, zp
+
+
 # ---- a5: group-wise weight quantization + linear layer --------------------------------------
 
 def quantize_weights(W: np.ndarray, bits: int = 4, group: int = 128):
