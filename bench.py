@@ -9,7 +9,7 @@ Multi-GPU (--gpus N, launched by torch.distributed.run): token-parallel replicas
 its own M = 4096 tokens and a replica of the 8 MiB int4 weight (linear layers are per-token, so no
 data-path collective exists); value = total tokens over all ranks / max-over-ranks time
 ("scaling": "weak").  The hidden-dim (tensor-parallel) variant with RCCL lives in
-diffusion-llm-rs_amd/parallel_linear.py (see DESIGN.md section Multi-GPU).
+diffusion-llm-rs_amd/parallel.py (see DESIGN.md section Multi-GPU).
 """
 from __future__ import annotations
 

@@ -1,0 +1,168 @@
+// linear_common.hpp -- pieces shared by the group-quantized GEMM kernels (linear_wq.hip,
+// linear_pp.hip): operand types, the fused p_sample epilogue, fragment dequant, output stores,
+// the LDS stage layout of the 256-row ring kernels.  Weight layouts: see linear_wq.hip.
+#pragma once
+#include "common.hpp"
+#include "diffusion_rng.hpp"
+
+typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+typedef float float16_t __attribute__((ext_vector_type(16)));
+
+namespace dllm {
+
+// Fused p_sample epilogue (dllm_linear_forward_psample): eps = acc + bias (f32) becomes
+// x_prev = (c1 x_t + c2 eps) + std * n, n = stream element offset + m N + n (or 0).
+struct PSampleEpi {
+    const float *x_t;
+    const float *coef;    // [M / rps][3]
+    int rps;              // rows per sample
+    int add;
+    uint64_t seed, offset;
+    float *x_prev;
+    const float *noise;   // precomputed noise [M][N] (e.g. drawn on a side stream), or null: in-lane
+};
+
+namespace {
+
+constexpr int kBM = 256, kBN = 128, kBK = 64, kThreads = 256;
+
+// Four consecutive outputs (m, n..n+3) of the fused epilogue; N % 4 == 0, offset % 4 == 0.
+__device__ __forceinline__ void psample4(const PSampleEpi &e, int m, int n, int N, float e0, float e1, float e2,
+                                         float e3) {
+    const size_t i = static_cast<size_t>(m) * N + n;
+    const float *c = e.coef + 3 * (m / e.rps);
+    const float c1 = c[0], c2 = c[1], sd = c[2];
+    float z[4] = {0.f, 0.f, 0.f, 0.f};
+    if (e.add) {
+        if (e.noise) {
+            const float4 nv = *reinterpret_cast<const float4 *>(e.noise + i);
+            z[0] = nv.x; z[1] = nv.y; z[2] = nv.z; z[3] = nv.w;
+        } else {
+            rng::normal4(e.seed, (e.offset + i) / 4, z);
+        }
+    }
+    const float4 x = *reinterpret_cast<const float4 *>(e.x_t + i);
+    float4 o;
+    o.x = (c1 * x.x + c2 * e0) + sd * z[0];
+    o.y = (c1 * x.y + c2 * e1) + sd * z[1];
+    o.z = (c1 * x.z + c2 * e2) + sd * z[2];
+    o.w = (c1 * x.w + c2 * e3) + sd * z[3];
+    *reinterpret_cast<float4 *>(e.x_prev + i) = o;
+}
+
+// Dequantizes the A fragment (8 f16) of substep s from a lane's slab words.
+template <int BITS>
+__device__ __forceinline__ half8_t dequant_frag(const uint32_t (&w)[BITS], int s, half2_t nz, half2_t sc) {
+    constexpr int PPW = 16 / BITS;
+    constexpr uint32_t mask2 = ((1u << BITS) - 1u) * 0x00010001u;
+    half8_t r;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        const int P = s * 4 + v;
+        const uint32_t word = w[P / PPW];
+        const uint32_t t = ((word >> (BITS * (P % PPW))) & mask2) | 0x64006400u;
+        half2_t h = __builtin_bit_cast(half2_t, t);
+        h = h + nz;        // exact: q - zp
+        h = h * sc;        // one f16 rounding of (q - zp) * scale
+        r[2 * v] = h[0];
+        r[2 * v + 1] = h[1];
+    }
+    return r;
+}
+
+__device__ __forceinline__ void split_sz(uint32_t szv, half2_t &nz, half2_t &sc) {
+    half2_t p = __builtin_bit_cast(half2_t, szv);
+    nz = half2_t{p[0], p[0]};
+    sc = half2_t{p[1], p[1]};
+}
+
+__device__ __forceinline__ void glds16(const void *gsrc, void *ldst) {
+    __builtin_amdgcn_global_load_lds((gbl_void_ptr)(const_cast<void *>(gsrc)), (lds_void_ptr)(ldst), 16, 0, 0);
+}
+
+template <typename YT>
+__device__ __forceinline__ void store4(YT *p, float a, float b, float c, float d);
+template <>
+__device__ __forceinline__ void store4<float>(float *p, float a, float b, float c, float d) {
+    *reinterpret_cast<float4 *>(p) = make_float4(a, b, c, d);
+}
+template <>
+__device__ __forceinline__ void store4<__half>(__half *p, float a, float b, float c, float d) {
+    union { __half h[4]; uint2 u; } pk;
+    pk.h[0] = __float2half_rn(a); pk.h[1] = __float2half_rn(b);
+    pk.h[2] = __float2half_rn(c); pk.h[3] = __float2half_rn(d);
+    *reinterpret_cast<uint2 *>(p) = pk.u;
+}
+template <typename YT>
+__device__ __forceinline__ void store1(YT *p, float a);
+template <>
+__device__ __forceinline__ void store1<float>(float *p, float a) { *p = a; }
+template <>
+__device__ __forceinline__ void store1<__half>(__half *p, float a) { *p = __float2half_rn(a); }
+
+// Stores 4 consecutive outputs y[n..n+3] (+ bias), masking n >= N.
+template <typename YT>
+__device__ __forceinline__ void store_out4(YT *yrow, const float *__restrict__ bias, int n, int N, bool vec_ok,
+                                           float a0, float a1, float a2, float a3) {
+    if (n >= N) return;
+    const float4 bv = *reinterpret_cast<const float4 *>(bias + n);
+    const float y0 = a0 + bv.x, y1 = a1 + bv.y, y2 = a2 + bv.z, y3 = a3 + bv.w;
+    if (vec_ok) {
+        store4<YT>(yrow + n, y0, y1, y2, y3);
+    } else {
+        store1<YT>(yrow + n, y0);
+        if (n + 1 < N) store1<YT>(yrow + n + 1, y1);
+        if (n + 2 < N) store1<YT>(yrow + n + 2, y2);
+        if (n + 3 < N) store1<YT>(yrow + n + 3, y3);
+    }
+}
+
+constexpr int kMReps = kBM / 32;   // 8
+
+
+template <int BITS>
+__device__ __forceinline__ void lds_words(uint32_t (&w)[BITS], const uint8_t *wbase, int lane) {
+    if constexpr (BITS == 4) {
+        uint4 v = *reinterpret_cast<const uint4 *>(wbase + lane * 16);
+        w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+    } else if constexpr (BITS == 8) {
+        uint4 a = *reinterpret_cast<const uint4 *>(wbase + lane * 16);
+        uint4 b = *reinterpret_cast<const uint4 *>(wbase + 64 * 16 + lane * 16);
+        w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+    } else {
+        w[0] = *reinterpret_cast<const uint32_t *>(wbase + lane * 4);
+        w[1] = *reinterpret_cast<const uint32_t *>(wbase + 256 + lane * 4);
+    }
+}
+
+
+// LDS-DMA issued from inline asm: invisible to hipcc's waitcnt pass, so the only waits on these
+// loads are the counted vmcnt statements placed by hand (guide 5.7, M0 written in the statement).
+template <int BITS, int NW = 8, int MR = kMReps, int KG = 1>
+struct StageLayout8 {
+    static constexpr int kWaves = NW * KG;
+    static constexpr int kXRounds = 4 * MR / kWaves;      // 1-KiB wave-instructions per wave for X
+    static constexpr int kX = 32 * MR * kBK * 2;
+    static constexpr int kW = NW * 64 * BITS * 4;
+    static constexpr int kSZ = NW * 64 * 4;
+    static constexpr int kBytes = kX + kW + kSZ;
+    static constexpr int kWOps = BITS == 4 ? 1 : 2;
+    // LDS-DMA instructions per wave per stage.  KG = 1: X rounds + weight words + 1 scale dword.
+    // KG = 2: k-group 0 loads the weight words, k-group 1 the scales.
+    static constexpr int kOps0 = kXRounds + kWOps + (KG == 1 ? 1 : 0);
+    static constexpr int kOps1 = kXRounds + 1;
+};
+
+
+}  // namespace
+
+// Ping-pong 256 x 256 GEMM (linear_pp.hip): Y = X . W^ + b for the 256-column-tile grid, bits in
+// {2, 4, 8}, Y f16 (y_f32 = 0) or f32, epi != null: fused p_sample epilogue into epi->x_prev.
+// sched: 1 / 2 = 32x32x16 MFMA, 1 or 2 16-deep substeps per phase (wdev = prefill layout);
+// 3 = 16x16x32 MFMA (wdev = the w16 layout).  lab: ablation mask (measurement only, 0 in production).
+int launch_pp_gemm(int bits, int y_f32, const __half *X, int M, int K, const uint32_t *wdev, const uint32_t *sz,
+                   const float *bias, void *Y, int N, int Npad, int group, int sched, const PSampleEpi *epi,
+                   hipStream_t st, int lab = 0);
+
+}  // namespace dllm

@@ -16,7 +16,7 @@
 //   ((word >> bits*p) & mask2) | 0x64006400 is the f16 pair (1024 + q_2v, 1024 + q_2v+1).
 //   Per (group, column) one u32 `sz` = f16 pair {-(1024 + zp), f16(scale)}:
 //   f16(q - zp) is exact (|q - zp| < 2048), then one f16 rounding of (q - zp) * f16(scale).
-#include "common.hpp"
+#include "linear_common.hpp"
 #include "diffusion_rng.hpp"
 
 #include <algorithm>
@@ -25,10 +25,8 @@
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <type_traits>
 
-typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
-typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
-typedef float float16_t __attribute__((ext_vector_type(16)));
 
 struct dllm_linear {
     size_t K = 0, N = 0, Npad = 0, G = 0, group = 0;
@@ -47,49 +45,14 @@ struct dllm_linear {
     int variant = 4;              // prefill schedule variant (tuning knob, see wq_gemm_kernel)
     int dlab = 0;                 // decode-kernel ablation mask (measurement only; 0 in production)
     int rlab = 0;                 // ring-kernel ablation mask (measurement only; 0 in production)
+    int pplab = 0;                // ping-pong-kernel ablation mask (measurement only; 0 in production)
     std::mutex mu;
 };
 
 namespace dllm {
 namespace {
 
-constexpr int kBM = 256, kBN = 128, kBK = 64, kThreads = 256;
 
-// Fused p_sample epilogue (dllm_linear_forward_psample): eps = acc + bias (f32) becomes
-// x_prev = (c1 x_t + c2 eps) + std * n, n = stream element offset + m N + n (or 0).
-struct PSampleEpi {
-    const float *x_t;
-    const float *coef;    // [M / rps][3]
-    int rps;              // rows per sample
-    int add;
-    uint64_t seed, offset;
-    float *x_prev;
-    const float *noise;   // precomputed noise [M][N] (e.g. drawn on a side stream), or null: in-lane
-};
-
-// Four consecutive outputs (m, n..n+3) of the fused epilogue; N % 4 == 0, offset % 4 == 0.
-__device__ __forceinline__ void psample4(const PSampleEpi &e, int m, int n, int N, float e0, float e1, float e2,
-                                         float e3) {
-    const size_t i = static_cast<size_t>(m) * N + n;
-    const float *c = e.coef + 3 * (m / e.rps);
-    const float c1 = c[0], c2 = c[1], sd = c[2];
-    float z[4] = {0.f, 0.f, 0.f, 0.f};
-    if (e.add) {
-        if (e.noise) {
-            const float4 nv = *reinterpret_cast<const float4 *>(e.noise + i);
-            z[0] = nv.x; z[1] = nv.y; z[2] = nv.z; z[3] = nv.w;
-        } else {
-            rng::normal4(e.seed, (e.offset + i) / 4, z);
-        }
-    }
-    const float4 x = *reinterpret_cast<const float4 *>(e.x_t + i);
-    float4 o;
-    o.x = (c1 * x.x + c2 * e0) + sd * z[0];
-    o.y = (c1 * x.y + c2 * e1) + sd * z[1];
-    o.z = (c1 * x.z + c2 * e2) + sd * z[2];
-    o.w = (c1 * x.w + c2 * e3) + sd * z[3];
-    *reinterpret_cast<float4 *>(e.x_prev + i) = o;
-}
 
 inline size_t canon_words(size_t K, size_t N, int bits) { return (K * N * bits + 31) / 32; }
 
@@ -280,75 +243,6 @@ __device__ __forceinline__ void load_words(uint32_t (&w)[BITS], const uint32_t *
     }
 }
 
-// Dequantizes the A fragment (8 f16) of substep s from a lane's slab words.
-template <int BITS>
-__device__ __forceinline__ half8_t dequant_frag(const uint32_t (&w)[BITS], int s, half2_t nz, half2_t sc) {
-    constexpr int PPW = 16 / BITS;
-    constexpr uint32_t mask2 = ((1u << BITS) - 1u) * 0x00010001u;
-    half8_t r;
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-        const int P = s * 4 + v;
-        const uint32_t word = w[P / PPW];
-        const uint32_t t = ((word >> (BITS * (P % PPW))) & mask2) | 0x64006400u;
-        half2_t h = __builtin_bit_cast(half2_t, t);
-        h = h + nz;        // exact: q - zp
-        h = h * sc;        // one f16 rounding of (q - zp) * scale
-        r[2 * v] = h[0];
-        r[2 * v + 1] = h[1];
-    }
-    return r;
-}
-
-__device__ __forceinline__ void split_sz(uint32_t szv, half2_t &nz, half2_t &sc) {
-    half2_t p = __builtin_bit_cast(half2_t, szv);
-    nz = half2_t{p[0], p[0]};
-    sc = half2_t{p[1], p[1]};
-}
-
-__device__ __forceinline__ void glds16(const void *gsrc, void *ldst) {
-    __builtin_amdgcn_global_load_lds((gbl_void_ptr)(const_cast<void *>(gsrc)), (lds_void_ptr)(ldst), 16, 0, 0);
-}
-
-template <typename YT>
-__device__ __forceinline__ void store4(YT *p, float a, float b, float c, float d);
-template <>
-__device__ __forceinline__ void store4<float>(float *p, float a, float b, float c, float d) {
-    *reinterpret_cast<float4 *>(p) = make_float4(a, b, c, d);
-}
-template <>
-__device__ __forceinline__ void store4<__half>(__half *p, float a, float b, float c, float d) {
-    union { __half h[4]; uint2 u; } pk;
-    pk.h[0] = __float2half_rn(a); pk.h[1] = __float2half_rn(b);
-    pk.h[2] = __float2half_rn(c); pk.h[3] = __float2half_rn(d);
-    *reinterpret_cast<uint2 *>(p) = pk.u;
-}
-template <typename YT>
-__device__ __forceinline__ void store1(YT *p, float a);
-template <>
-__device__ __forceinline__ void store1<float>(float *p, float a) { *p = a; }
-template <>
-__device__ __forceinline__ void store1<__half>(__half *p, float a) { *p = __float2half_rn(a); }
-
-// Stores 4 consecutive outputs y[n..n+3] (+ bias), masking n >= N.
-template <typename YT>
-__device__ __forceinline__ void store_out4(YT *yrow, const float *__restrict__ bias, int n, int N, bool vec_ok,
-                                           float a0, float a1, float a2, float a3) {
-    if (n >= N) return;
-    const float4 bv = *reinterpret_cast<const float4 *>(bias + n);
-    const float y0 = a0 + bv.x, y1 = a1 + bv.y, y2 = a2 + bv.z, y3 = a3 + bv.w;
-    if (vec_ok) {
-        store4<YT>(yrow + n, y0, y1, y2, y3);
-    } else {
-        store1<YT>(yrow + n, y0);
-        if (n + 1 < N) store1<YT>(yrow + n + 1, y1);
-        if (n + 2 < N) store1<YT>(yrow + n + 2, y2);
-        if (n + 3 < N) store1<YT>(yrow + n + 3, y3);
-    }
-}
-
-constexpr int kMReps = kBM / 32;   // 8
-
 // LDS stage layout (bytes): X tile [256][64] f16 (32 KiB) | W slabs [4 waves][64 lanes][BITS words]
 // | sz [4 waves][64 lanes] u32.  Everything arrives by global_load_lds, so hipcc's counters see no
 // register-destination global load in the loop (mixing the two kinds makes it wait vmcnt(0) at
@@ -373,21 +267,6 @@ __device__ __forceinline__ void glds_words(const uint32_t *gsrc, uint8_t *ldst) 
         __builtin_amdgcn_global_load_lds((gbl_void_ptr)(const_cast<uint32_t *>(gsrc)), (lds_void_ptr)(ldst), 4, 0, 0);
         __builtin_amdgcn_global_load_lds((gbl_void_ptr)(const_cast<uint32_t *>(gsrc + 1)), (lds_void_ptr)(ldst + 256),
                                          4, 0, 0);
-    }
-}
-
-template <int BITS>
-__device__ __forceinline__ void lds_words(uint32_t (&w)[BITS], const uint8_t *wbase, int lane) {
-    if constexpr (BITS == 4) {
-        uint4 v = *reinterpret_cast<const uint4 *>(wbase + lane * 16);
-        w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
-    } else if constexpr (BITS == 8) {
-        uint4 a = *reinterpret_cast<const uint4 *>(wbase + lane * 16);
-        uint4 b = *reinterpret_cast<const uint4 *>(wbase + 64 * 16 + lane * 16);
-        w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
-    } else {
-        w[0] = *reinterpret_cast<const uint32_t *>(wbase + lane * 4);
-        w[1] = *reinterpret_cast<const uint32_t *>(wbase + 256 + lane * 4);
     }
 }
 
@@ -583,23 +462,6 @@ wq_gemm_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__res
 // while kt is computed, the end-of-step wait is a COUNTED vmcnt that leaves kt+2's DMAs in flight
 // across the raw s_barrier (never __syncthreads, whose fence would drain them).
 // ---------------------------------------------------------------------------------------------
-// LDS-DMA issued from inline asm: invisible to hipcc's waitcnt pass, so the only waits on these
-// loads are the counted vmcnt statements placed by hand (guide 5.7, M0 written in the statement).
-template <int BITS, int NW = 8, int MR = kMReps, int KG = 1>
-struct StageLayout8 {
-    static constexpr int kWaves = NW * KG;
-    static constexpr int kXRounds = 4 * MR / kWaves;      // 1-KiB wave-instructions per wave for X
-    static constexpr int kX = 32 * MR * kBK * 2;
-    static constexpr int kW = NW * 64 * BITS * 4;
-    static constexpr int kSZ = NW * 64 * 4;
-    static constexpr int kBytes = kX + kW + kSZ;
-    static constexpr int kWOps = BITS == 4 ? 1 : 2;
-    // LDS-DMA instructions per wave per stage.  KG = 1: X rounds + weight words + 1 scale dword.
-    // KG = 2: k-group 0 loads the weight words, k-group 1 the scales.
-    static constexpr int kOps0 = kXRounds + kWOps + (KG == 1 ? 1 : 0);
-    static constexpr int kOps1 = kXRounds + 1;
-};
-
 // Ring GEMM: block tile (32 MR) x (32 NW), NW*KG waves.  Wave (cw, kg) = (wave % NW, wave / NW)
 // owns output columns n0 + 32 cw .. +32 for all 32 MR rows and, of every 64-deep k-step, the
 // 4/KG substeps kg*4/KG ..: KG = 2 puts two waves on each SIMD at the same tile count (the 128-row
@@ -1542,6 +1404,10 @@ int launch_auto(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t
     const int np = static_cast<int>(h->Npad);
     const int mb256 = (M + 255) / 256, mb128 = (M + 127) / 128;
     if (np % 256 == 0 && mb256 * (np / 256) >= kCUs) {
+        if (h->variant >= 9 && h->variant <= 11)   // ping-pong schedules (linear_pp.hip)
+            return launch_pp_gemm(BITS, std::is_same<YT, float>::value ? 1 : 0, X, M, (int)h->K,
+                                  h->variant == 11 ? h->w16 : h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad,
+                                  (int)h->group, h->variant - 8, EPI ? epi : nullptr, st, h->pplab);
         if (h->variant == 8) {
             const PSampleEpi ep = epi ? *epi : PSampleEpi{};
             wq_gemm16_kernel<BITS, YT, EPI><<<static_cast<unsigned>(mb256 * (np / 256)), 512, 0, st>>>(
@@ -1574,7 +1440,7 @@ int launch_auto(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t
 template <int BITS, typename YT>
 int launch_gemm_t(const dllm_linear *h, const __half *X, size_t M, YT *Y, hipStream_t st) {
     if (M <= static_cast<size_t>(kDecodeMaxM)) return launch_decode<BITS, YT>(h, X, M, Y, st);
-    if (h->variant == 4 || h->variant == 5 || h->variant == 7 || h->variant == 8)
+    if (h->variant == 4 || h->variant == 5 || h->variant >= 7)
         return launch_auto<BITS, YT>(h, X, (int)M, Y, st);
     if (h->variant == 6) {   // previous policy: 2-stage kernels, 128-row tiles + split below 256 tiles
         const int tiles256 = static_cast<int>((M + kBM - 1) / kBM) * static_cast<int>(h->Npad / kBN);
@@ -1768,7 +1634,7 @@ int dllm_linear_forward_psample(dllm_linear_t h, const void *X, size_t M, int x_
     const __half *Xh = nullptr;
     if (const int rc = prepare_x(h, X, M, x_dtype, st, &Xh)) return rc;
     if (M <= static_cast<size_t>(kDecodeMaxM) ||
-        (h->variant != 4 && h->variant != 5 && h->variant != 7 && h->variant != 8)) {
+        (h->variant != 4 && h->variant != 5 && h->variant < 7)) {
         // Paths without the fused epilogue: f32 eps through a per-stream workspace, then p_sample
         // (the same eps bits, hence the same result as the fused form on that path).
         float *eps = device_workspace(st, M * h->N * sizeof(float), 1);
@@ -1834,9 +1700,15 @@ int dllm_linear_set_kernel_variant(dllm_linear_t h, int variant) {
         h->rlab = variant - 32;
         return DLLM_OK;
     }
-    if (variant < 0 || variant > 8) return fail(DLLM_ERR_INVALID_PARAMS, "variant must be 0..8 (16..23, 32..95: ablations)");
+    if (variant >= 100 && variant < 196) {   // ping-pong ablation: 100 / 132 / 164 + lab -> variant 9 / 10 / 11
+        h->variant = 9 + (variant - 100) / 32;
+        h->pplab = (variant - 100) % 32;
+        return DLLM_OK;
+    }
+    if (variant < 0 || variant > 11)
+        return fail(DLLM_ERR_INVALID_PARAMS, "variant must be 0..11 (16..23, 32..95, 100..195: ablations)");
     h->variant = variant;
-    h->dlab = h->rlab = 0;
+    h->dlab = h->rlab = h->pplab = 0;
     return DLLM_OK;
 }
 

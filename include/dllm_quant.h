@@ -186,8 +186,10 @@ int dllm_linear_info(dllm_linear_t h, size_t *K, size_t *N, uint8_t *bits, size_
 size_t dllm_linear_weight_bytes(dllm_linear_t h);
 /* Tuning knob (benchmarks / A-B runs).  4 (default): tile policy over the 3-stage-ring kernels
  * (256x256, 256x128, 128x128 + split-K); 5: same; 0..3: the 2-stage 256x128 schedules;
- * 6: 2-stage kernels with 128-row tiles + split-K below 256 tiles; 16..23: decode-kernel
- * ablation mask (measurement only: replaces loads by constants, results are garbage). */
+ * 6: 2-stage kernels with 128-row tiles + split-K below 256 tiles; 7: 256x256 tile, 2x4 waves;
+ * 8: 256x256 tile on the 16x16x32 MFMA; 9/10: ping-pong wave groups (1/2 substeps per phase);
+ * 11: ping-pong on the 16x16x32 MFMA.  16..23, 32..95, 100..195: ablation masks of the decode,
+ * ring and ping-pong kernels (measurement only: loads or math replaced, results are garbage). */
 int dllm_linear_set_kernel_variant(dllm_linear_t h, int variant);
 int dllm_linear_destroy(dllm_linear_t h);
 

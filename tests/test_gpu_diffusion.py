@@ -108,6 +108,18 @@ def test_linear_psample_fused_bit_identical(dllm, cuda, M, K, N, rps):
     xt2 = xt.clone()
     lin.forward_psample(X, xt2, coef, rps, flag, seed=5, offset=16, out=xt2)
     assert torch.equal(xt2.view(torch.int32), ref.view(torch.int32))
+    if M == 4096:   # the other 256x256 kernels: fused epilogue vs their own eps + p_sample
+        for v in (8, 9, 10, 11):
+            lin.set_kernel_variant(v)
+            fv = lin.forward_psample(X, xt, coef, rps, flag, seed=5, offset=16)
+            ev = lin(X, out_dtype=torch.float32)
+            rv = torch.empty_like(xt)
+            dllm._lib.check(lib.dllm_p_sample(C.c_void_p(xt.data_ptr()), C.c_void_p(ev.data_ptr()), None,
+                                              C.c_void_p(row_coef.data_ptr()), M, N, int(flag), 5, 16,
+                                              C.c_void_p(rv.data_ptr()),
+                                              C.c_void_p(torch.cuda.current_stream().cuda_stream)))
+            torch.cuda.synchronize()
+            assert torch.equal(fv.view(torch.int32), rv.view(torch.int32)), v
     lin.close()
 
 

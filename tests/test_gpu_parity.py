@@ -321,11 +321,12 @@ def test_linear_split_k_exact_integers(dllm, torch, orc):
     assert np.array_equal(Y, (X.astype(np.float64) @ W.astype(np.float64)).astype(np.float32))
 
 
-@pytest.mark.parametrize("variant", [4, 8])
+@pytest.mark.parametrize("variant", [4, 8, 9, 10, 11])
 @pytest.mark.parametrize("bits", [2, 4, 8])
 def test_linear_big_tile_exact_integers(dllm, torch, orc, variant, bits):
     """256x256-tile kernels (variant 4: 32x32x16 MFMA, w-layout; variant 8: 16x16x32 MFMA, w16
-    layout) on exact-integer data at M = N = 4096 (K = 256, so the f16 products and f32 sums are
+    layout; 9/10: the ping-pong schedule, 1 or 2 substeps per phase; 11: ping-pong on 16x16x32) on
+    exact-integer data at M = N = 4096 (K = 256, so the f16 products and f32 sums are
     exact): the result must equal the f64 product bit for bit, catching any fragment-map error."""
     K, N, M = 256, 4096, 4096
     rng = np.random.default_rng(31 + bits)
@@ -422,15 +423,25 @@ def test_host_entry_points(dllm, orc):
 
 def test_gemm_variants_bit_identical(dllm, torch):
     """All prefill schedules (0..3: 256x128 tile; 4: 256x256 tile, 3-stage LDS ring, 1x8 waves;
-    7: the same tile with 2x4 waves) accumulate every output in the same k order, so they must
-    agree bit for bit -- including a ragged M tail."""
+    7: the same tile with 2x4 waves; 9/10: ping-pong wave groups) accumulate every output in the
+    same k order, so they must agree bit for bit -- including a ragged M tail -- for f32 and f16
+    outputs."""
     K, N, M = 1024, 4096, 4352
     g = torch.Generator(device="cuda").manual_seed(8)
     W = 0.02 * torch.randn(K, N, device="cuda", generator=g)
     X = torch.randn(M, K, device="cuda", generator=g).half()
     lin = dllm.QuantLinear.from_weight(W, 0.1 * torch.randn(N, device="cuda", generator=g), 4, 128)
-    outs = {}
-    for v in (0, 3, 4, 7):
+    outs, outs16 = {}, {}
+    for v in (0, 3, 4, 7, 9, 10):
         lin.set_kernel_variant(v)
         outs[v] = lin(X, out_dtype=torch.float32)
-    assert torch.equal(outs[0], outs[3]) and torch.equal(outs[0], outs[4]) and torch.equal(outs[0], outs[7])
+        outs16[v] = lin(X, out_dtype=torch.float16)
+    for v in (3, 4, 7, 9, 10):
+        assert torch.equal(outs[0], outs[v]), v
+        assert torch.equal(outs16[0], outs16[v]), v
+    # the 16x16x32 kernels sum 32-deep MFMA chunks: equal to each other, not to the 32x32x16 ones
+    for v in (8, 11):
+        lin.set_kernel_variant(v)
+        outs[v] = lin(X, out_dtype=torch.float32)
+        outs16[v] = lin(X, out_dtype=torch.float16)
+    assert torch.equal(outs[8], outs[11]) and torch.equal(outs16[8], outs16[11])
