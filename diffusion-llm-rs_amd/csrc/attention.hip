@@ -364,6 +364,240 @@ kv_attention_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__ 
     }
 }
 
+
+// Row reductions across the two lane halves (lane l and l ^ 32 hold the two key halves of one
+// query): v_permlane32_swap (VALU) instead of a ds_bpermute round trip through the LDS unit.
+// Both halves compute the same expression of the same two values, so they agree bit for bit.
+__device__ __forceinline__ float swap_halves_max(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float swap_halves_sum(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// v5: the same algorithm and LDS ring as kv_attention_kernel with an explicit in-wave schedule:
+// S^T of block kb+1 and the softmax of block kb share one scheduling region, the MFMAs paced by
+// sched_group_barrier with softmax VALU and K-fragment reads in their gaps (hipcc had issued the
+// 16 QK MFMAs back to back and then the whole softmax); the max and sum reductions are trees
+// (depth 5 instead of 32-long chains); the k-loop is unrolled by two so the score register sets
+// swap roles instead of being copied.
+template <int LAB = 0>
+__global__ void __launch_bounds__(kWaves * 64)
+kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__ img, const float *__restrict__ kp,
+                    const float *__restrict__ vp, int S, int H, _Float16 *__restrict__ O) {
+    const int nkb = (S + kKB - 1) / kKB;
+    __shared__ __attribute__((aligned(16))) AttnSmem sm;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h = blockIdx.y;
+    const int q0 = blockIdx.x * kQT + wave * 32;
+    const int ql = lane & 31, hh = lane >> 5;
+    const float ks = kp[0], vs = vp[0];
+    // exp2 domain, K scale folded in: p = exp2(c * raw - m), c = log2(e) * s_k / sqrt(D).
+    const float c = 1.4426950408889634f * ks / sqrtf(static_cast<float>(kD));
+
+    // Q^T fragments (B operand of S^T = K Q^T): lane holds Q[q = q0 + ql][d = 16 t + 8 hh + j].
+    half8_t qf[kD / 16];
+    {
+        const int qrow = min(q0 + ql, S - 1);
+        const _Float16 *qp = Q + (static_cast<size_t>(qrow) * H + h) * kD + 8 * hh;
+#pragma unroll
+        for (int t = 0; t < kD / 16; ++t) qf[t] = *reinterpret_cast<const half8_t *>(qp + 16 * t);
+    }
+
+    float16_t o[kD / 32];   // O tiles: d-tile dt, lane = d (within tile), rows = query via regs
+#pragma unroll
+    for (int dt = 0; dt < kD / 32; ++dt)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) o[dt][e] = 0.0f;
+    float m_run = -INFINITY, l_run = 0.0f;   // for query q0 + ql (same in both lane halves)
+
+    // S^T (2 x 32 keys x 32 queries) of a staged K block: st[u][r] is key 32u + (r&3) + 8(r>>2) + 4hh
+    // of the block, query q0 + ql.
+    auto qk = [&](float16_t (&st)[2], const _Float16 (&kb_)[kKB][kKRow]) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) st[u][e] = 0.0f;
+#pragma unroll
+            for (int t = 0; t < kD / 16; ++t) {
+                const half8_t kf = *reinterpret_cast<const half8_t *>(&kb_[32 * u + ql][16 * t + 8 * hh]);
+                st[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[t], st[u], 0, 0, 0);
+            }
+        }
+    };
+
+    // LDS-DMA of the workspace images: wave w moves pieces w, w + 8, ... (1 KiB each).
+    const uint8_t *himg = img + static_cast<size_t>(h) * nkb * kImg + lane * 16;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(wave);
+    auto dma_k = [&](int blk, int buf) {
+        const uint8_t *src = himg + static_cast<size_t>(blk) * kImg;
+        const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_addr(&sm.k[buf][0][0]));
+        for (uint32_t p = wv; p < kKImg / 1024; p += kWaves) glds16_asm(src + p * 1024, dst + p * 1024);
+    };
+    auto dma_v = [&](int blk, int buf) {
+        const uint8_t *src = himg + static_cast<size_t>(blk) * kImg + kKImg;
+        const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_addr(&sm.vt[buf][0][0]));
+        for (uint32_t p = wv; p < kVImg / 1024; p += kWaves) glds16_asm(src + p * 1024, dst + p * 1024);
+    };
+    // Prologue: K and V of block 0 and K of block 1 staged; S^T of block 0 computed.
+    dma_k(0, 0);
+    dma_v(0, 0);
+    if (nkb > 1) dma_k(1, 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // One k-block: DMAs of the blocks ahead, then region 1 (S^T of block kb+1 on the matrix pipe,
+    // the softmax of block kb on the VALU in the MFMA gaps), the O rescale (rare), region 2 (P V of
+    // block kb with the V fragment reads and the P conversion in the gaps), one barrier.  The
+    // scores of the next block land in `sn`; the caller swaps the two register sets.
+    auto iter = [&](float16_t (&st)[2], float16_t (&sn)[2], int kb) {
+        const int j0 = kb * kKB;
+        const bool more1 = kb + 1 < nkb, more2 = kb + 2 < nkb;
+        if (!(LAB & 2)) {
+            if (more2) dma_k(kb + 2, kb & 1);
+            if (more1) dma_v(kb + 1, (kb + 1) & 1);
+        }
+        if (__builtin_expect(j0 + kKB > S, 0)) {   // last, partial block only (a real branch)
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int key = j0 + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * hh;
+                    st[u][r] = key < S ? st[u][r] : -INFINITY;
+                }
+        }
+        // ---- region 1.  After the last block the K buffer is stale: sn is computed and dropped.
+        const auto &kn = sm.k[(kb + 1) & 1];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) sn[u][e] = 0.0f;
+#pragma unroll
+            for (int t = 0; t < kD / 16; ++t) {
+                const half8_t kf = *reinterpret_cast<const half8_t *>(&kn[32 * u + ql][16 * t + 8 * hh]);
+                if constexpr (LAB & 8) {   // measurement only: no QK MFMAs (reads kept live)
+                    asm volatile("" ::"v"(kf));
+                    sn[u][t] += 1.0f;
+                } else {
+                    sn[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[t], sn[u], 0, 0, 0);
+                }
+            }
+        }
+        float alpha = 1.0f;
+        if constexpr (LAB & 1) {   // measurement only: no softmax (P = raw scores)
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(st[u][r]));
+        } else {
+        float mt[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mt[r] = fmaxf(st[0][r], st[1][r]);
+#pragma unroll
+        for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+            for (int r = 0; r < w; ++r) mt[r] = fmaxf(mt[r], mt[r + w]);
+        const float mloc = swap_halves_max(mt[0]);
+        const float m_new = fmaxf(m_run, mloc * c);
+        // raw v_exp_f32 (P below 2^-126 is 0 in the f16 P anyway); exp2(0) = 1 exactly.
+        alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) st[u][r] = __builtin_amdgcn_exp2f(fmaf(st[u][r], c, -m_new));
+        m_run = m_new;
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 1);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+            __builtin_amdgcn_sched_group_barrier(0x002, 5, 1);
+        }
+        // ---- rescale O rows by their query's alpha, only if some query's max moved ----
+        if (!(LAB & 1) && !__all(alpha == 1.0f)) {
+            if (hh == 0) sm.bcast[wave][ql] = alpha;
+            __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float4 a4 = *reinterpret_cast<const float4 *>(&sm.bcast[wave][8 * g + 4 * hh]);
+#pragma unroll
+                for (int dt = 0; dt < kD / 32; ++dt) {
+                    o[dt][4 * g + 0] *= a4.x; o[dt][4 * g + 1] *= a4.y;
+                    o[dt][4 * g + 2] *= a4.z; o[dt][4 * g + 3] *= a4.w;
+                }
+            }
+        }
+        // ---- region 2: O += P (q_v - z_v), the P^T accumulator as the A operand ----
+        const auto &vt = sm.vt[kb & 1];
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+            const int u = s2 >> 1, sl = s2 & 1;
+            half8_t pa;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) pa[j] = static_cast<_Float16>(st[u][8 * sl + j]);
+#pragma unroll
+            for (int dt = 0; dt < kD / 32; ++dt) {
+                // element j <-> key 16s + 8(j>>2) + 4hh + (j&3), d = 32dt + ql
+                const _Float16 *vrow = &vt[32 * dt + ql][16 * s2 + 4 * hh];
+                const half4_t lo = *reinterpret_cast<const half4_t *>(vrow);
+                const half4_t hi = *reinterpret_cast<const half4_t *>(vrow + 8);
+                const half8_t vb = half8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                if constexpr (LAB & 4) {   // measurement only: no PV MFMAs (operands kept live)
+                    asm volatile("" ::"v"(vb), "v"(pa));
+                } else {
+                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(pa, vb, o[dt], 0, 0, 0);
+                }
+            }
+        }
+        // the row sum of P rides in region 2's gaps (only l_run needs it)
+        float ls[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) ls[r] = st[0][r] + st[1][r];
+#pragma unroll
+        for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+            for (int r = 0; r < w; ++r) ls[r] = ls[r] + ls[r + w];
+        l_run = l_run * alpha + swap_halves_sum(ls[0]);
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 2);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 2);
+            __builtin_amdgcn_sched_group_barrier(0x002, 5, 2);
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    };
+    float16_t sa[2], sb[2];
+    qk(sa, sm.k[0]);
+    for (int kb = 0; kb < nkb; kb += 2) {
+        iter(sa, sb, kb);
+        if (kb + 1 < nkb) iter(sb, sa, kb + 1);
+    }
+
+    // ---- normalise (1/l and the V scale) and store: o[dt][r] -> query q0 + (r&3) + 8(r>>2) + 4hh ----
+    if (hh == 0) sm.bcast[wave][ql] = vs / l_run;
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const float4 inv = *reinterpret_cast<const float4 *>(&sm.bcast[wave][8 * g + 4 * hh]);
+        const float iv[4] = {inv.x, inv.y, inv.z, inv.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int q = q0 + 8 * g + 4 * hh + i;
+            if (q >= S) continue;
+            _Float16 *op = O + (static_cast<size_t>(q) * H + h) * kD + ql;
+#pragma unroll
+            for (int dt = 0; dt < kD / 32; ++dt) op[32 * dt] = static_cast<_Float16>(o[dt][4 * g + i] * iv[i]);
+        }
+    }
+}
+
 }  // namespace
 }  // namespace dllm
 
@@ -393,7 +627,8 @@ extern "C" int dllm_kv_attention(const void *Q, const uint8_t *Kq, const float *
     DLLM_LAUNCH_CHECK();
     dim3 grid(static_cast<unsigned>((S + kQT - 1) / kQT), static_cast<unsigned>(H));
     // DLLM_ATTN_LAB (measurement only; results are garbage when set): 1 no softmax, 2 no K/V
-    // staging, 4 no PV MFMAs, 8 no QK MFMAs.
+    // staging, 4 no PV MFMAs, 8 no QK MFMAs (on the v4 kernel); 100: the v4 kernel itself (valid
+    // results); 100 + mask: the same masks on the v5 kernel.
     static const int lab = [] { const char *e = getenv("DLLM_ATTN_LAB"); return e ? atoi(e) : 0; }();
     const _Float16 *Qh = static_cast<const _Float16 *>(Q);
     _Float16 *Oh = static_cast<_Float16 *>(O);
@@ -402,7 +637,15 @@ extern "C" int dllm_kv_attention(const void *Q, const uint8_t *Kq, const float *
         DLLM_ALAB(1) DLLM_ALAB(2) DLLM_ALAB(3) DLLM_ALAB(4) DLLM_ALAB(5) DLLM_ALAB(6) DLLM_ALAB(7)
         DLLM_ALAB(8) DLLM_ALAB(12) DLLM_ALAB(13) DLLM_ALAB(14) DLLM_ALAB(15)
 #undef DLLM_ALAB
-        default: kv_attention_kernel<0><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh); break;
+        case 100:   // the v4 schedule (A/B)
+            kv_attention_kernel<0><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh);
+            break;
+#define DLLM_ALAB5(L) case 100 + L: kv_attention5_kernel<L><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh); break;
+        DLLM_ALAB5(1) DLLM_ALAB5(2) DLLM_ALAB5(4) DLLM_ALAB5(8) DLLM_ALAB5(12) DLLM_ALAB5(13) DLLM_ALAB5(3)
+#undef DLLM_ALAB5
+        default:
+            kv_attention5_kernel<0><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh);
+            break;
     }
     DLLM_LAUNCH_CHECK();
     return DLLM_OK;

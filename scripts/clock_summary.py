@@ -1,5 +1,5 @@
 """Per-kernel-template effective clock and MFMA cycle efficiency from scripts/clock_probe.sh output
-(GRBM_GUI_ACTIVE summed over the 8 XCDs / kernel-trace duration).  Usage: clock_summary.py DIR M [K N]"""
+(GRBM_GUI_ACTIVE summed over the 8 XCDs / kernel-trace duration).  Usage: clock_summary.py DIR M [K N] [FLOP]: FLOP overrides the GEMM's 2 M N K for the efficiency column."""
 import collections, csv, sys
 from pathlib import Path
 
@@ -7,21 +7,26 @@ d = Path(sys.argv[1])
 M = int(sys.argv[2])
 K = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
 N = int(sys.argv[4]) if len(sys.argv) > 4 else 4096
-rows = list(csv.DictReader(open(next(d.glob("*counter_collection.csv")))))
-tr = {r["Dispatch_Id"]: r for r in csv.DictReader(open(next(d.glob("*kernel_trace.csv"))))}
+rows, tr = [], {}
+for f in sorted(d.rglob("*counter_collection.csv")):
+    rows += [(f.parent, r) for r in csv.DictReader(open(f))]
+    for g in f.parent.glob("*kernel_trace.csv"):
+        tr.update({(f.parent, r["Dispatch_Id"]): r for r in csv.DictReader(open(g))})
 order, agg = [], collections.defaultdict(list)
-for r in rows:
-    t = tr.get(r["Dispatch_Id"])
+for parent, r in rows:
+    t = tr.get((parent, r["Dispatch_Id"]))
     if t is None:
         continue
     dur = (int(t["End_Timestamp"]) - int(t["Start_Timestamp"])) * 1e-9
     kn = r["Kernel_Name"]
-    name = kn[kn.index("::wq") + 2: kn.index(">(") + 1] if "::wq" in kn else kn[:60]
+    name = kn.split("(")[0] if kn.startswith("void ") else kn
+    name = name.replace("void ", "").replace("dllm::", "").replace("(anonymous namespace)::", "")
     key = (name, r["Grid_Size"])
     if key not in agg:
         order.append(key)
     agg[key].append((dur, float(r["Counter_Value"])))
-ideal = 2 * M * N * K / (256 * 4 * 1024)   # cycles per SIMD at the 32x32x16 f16 issue peak
+flop = float(sys.argv[5]) if len(sys.argv) > 5 else 2.0 * M * N * K
+ideal = flop / (256 * 4 * 1024)   # cycles per SIMD at the f16 MFMA issue peak
 for key in order:
     v = agg[key][2:] or agg[key]
     dur = sum(x[0] for x in v) / len(v)
