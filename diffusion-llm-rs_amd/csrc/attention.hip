@@ -34,6 +34,7 @@ typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
 typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
 typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
 typedef float float16_t __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
 namespace dllm {
 namespace {
@@ -98,6 +99,9 @@ __device__ __forceinline__ void load_raw(Raw<BITS> &r, __amdgpu_buffer_rsrc_t kr
     }
 }
 
+// Position of key k (0..15) within its 16-key group of the V image: bits 2 and 3 swapped.
+__host__ __device__ constexpr int kv_pos(int k) { return (k & 3) | ((k & 4) << 1) | ((k & 8) >> 1); }
+
 // Code c (0..7) of an 8-code group of the thread's raw words, as the f16 pair trick input.
 template <int BITS>
 __device__ __forceinline__ half2_t pair_qz(uint32_t lo_word_codes, int shift, half2_t nz) {
@@ -139,9 +143,13 @@ __device__ __forceinline__ void store_raw(const Raw<BITS> &r, _Float16 (&bk)[kKB
                 v[i][2 * p] = x[0];
                 v[i][2 * p + 1] = x[1];
             }
+        // transposed, 4 consecutive keys of one dim per 8-B store, at the key position of the V
+        // image: keys 4..7 and 8..11 of every 16 swap places (kv_pos), so that the 8 keys a PV
+        // fragment lane needs (16 s + 4 hh + {0..3, 8..11}) sit in one 16-B run.
+        const int kp4 = (k4 & ~15) | kv_pos(k4 & 15);
 #pragma unroll
-        for (int dd = 0; dd < 8; ++dd)   // transposed: 4 consecutive keys of one dim per 8-B store
-            *reinterpret_cast<half4_t *>(&bvt[d0 + dd][k4]) = half4_t{v[0][dd], v[1][dd], v[2][dd], v[3][dd]};
+        for (int dd = 0; dd < 8; ++dd)
+            *reinterpret_cast<half4_t *>(&bvt[d0 + dd][kp4]) = half4_t{v[0][dd], v[1][dd], v[2][dd], v[3][dd]};
     }
 }
 
@@ -326,9 +334,9 @@ kv_attention_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__ 
 #pragma unroll
             for (int dt = 0; dt < kD / 32; ++dt) {
                 // element j <-> key 16s + 8(j>>2) + 4hh + (j&3), d = 32dt + ql
-                const _Float16 *vrow = &vt[32 * dt + ql][16 * s2 + 4 * hh];
+                const _Float16 *vrow = &vt[32 * dt + ql][16 * s2 + 8 * hh];   // kv_pos layout
                 const half4_t lo = *reinterpret_cast<const half4_t *>(vrow);
-                const half4_t hi = *reinterpret_cast<const half4_t *>(vrow + 8);
+                const half4_t hi = *reinterpret_cast<const half4_t *>(vrow + 4);
                 const half8_t vb = half8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
                 o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(pa, vb, o[dt], 0, 0, 0);
             }
@@ -454,9 +462,32 @@ kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__
     auto iter = [&](float16_t (&st)[2], float16_t (&sn)[2], int kb) {
         const int j0 = kb * kKB;
         const bool more1 = kb + 1 < nkb, more2 = kb + 2 < nkb;
-        if (!(LAB & 2)) {
-            if (more2) dma_k(kb + 2, kb & 1);
-            if (more1) dma_v(kb + 1, (kb + 1) & 1);
+        // Staging of K(kb+2) and V(kb+1): LDS-DMA as in v4 (default), or (LAB & 64, A/B) register
+        // loads now and LDS writes at the end of the block (each wave owns the 1-KiB pieces wave,
+        // wave + 8, wave + 16 of each image: a plain 16-B load and a ds_write_b128 per piece).
+        // Measured at S 8192 H 32: LDS-DMA 1111 us, register staging 1176 us.
+        u32x4_t kr[3], vr[3];
+        if constexpr (!(LAB & 2)) {
+            if constexpr (!(LAB & 64)) {
+                if (more2) dma_k(kb + 2, kb & 1);
+                if (more1) dma_v(kb + 1, (kb + 1) & 1);
+            } else {
+                // Branch-free (a load under a branch makes hipcc wait for it at once): past the last
+                // block the last block is re-staged into a free buffer, and piece indices past an
+                // image's end repeat its last piece (several waves then store the same bytes).
+                const uint8_t *ks_ = himg + static_cast<size_t>(min(kb + 2, nkb - 1)) * kImg;
+                const uint8_t *vs_ = himg + static_cast<size_t>(min(kb + 1, nkb - 1)) * kImg + kKImg;
+                // The loads are inline asm so that hipcc, which would sink them next to their
+                // stores and wait for them there, leaves them where they are; their one wait
+                // (vmcnt(0), naming every destination) precedes the LDS stores at the block's end.
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    const uint8_t *kp_ = ks_ + min(static_cast<int>(wv) + 8 * i, kKImg / 1024 - 1) * 1024;
+                    const uint8_t *vp_ = vs_ + min(static_cast<int>(wv) + 8 * i, kVImg / 1024 - 1) * 1024;
+                    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(kr[i]) : "v"(kp_) : "memory");
+                    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(vr[i]) : "v"(vp_) : "memory");
+                }
+            }
         }
         if (__builtin_expect(j0 + kKB > S, 0)) {   // last, partial block only (a real branch)
             asm volatile("" ::: "memory");
@@ -542,10 +573,8 @@ kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__
 #pragma unroll
             for (int dt = 0; dt < kD / 32; ++dt) {
                 // element j <-> key 16s + 8(j>>2) + 4hh + (j&3), d = 32dt + ql
-                const _Float16 *vrow = &vt[32 * dt + ql][16 * s2 + 4 * hh];
-                const half4_t lo = *reinterpret_cast<const half4_t *>(vrow);
-                const half4_t hi = *reinterpret_cast<const half4_t *>(vrow + 8);
-                const half8_t vb = half8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                // one 16-B read: keys 16s + 4hh + {0..3, 8..11} are adjacent in the kv_pos layout
+                const half8_t vb = *reinterpret_cast<const half8_t *>(&vt[32 * dt + ql][16 * s2 + 8 * hh]);
                 if constexpr (LAB & 4) {   // measurement only: no PV MFMAs (operands kept live)
                     asm volatile("" ::"v"(vb), "v"(pa));
                 } else {
@@ -562,15 +591,28 @@ kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__
 #pragma unroll
             for (int r = 0; r < w; ++r) ls[r] = ls[r] + ls[r + w];
         l_run = l_run * alpha + swap_halves_sum(ls[0]);
-        __builtin_amdgcn_sched_group_barrier(0x100, 4, 2);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 2);
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x100, 2, 2);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 2);
             __builtin_amdgcn_sched_group_barrier(0x002, 5, 2);
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+        if constexpr (!(LAB & 2) && (LAB & 64)) {
+            asm volatile("s_waitcnt vmcnt(0)"
+                         : "+v"(kr[0]), "+v"(kr[1]), "+v"(kr[2]), "+v"(vr[0]), "+v"(vr[1]), "+v"(vr[2])
+                         :
+                         : "memory");
+            uint8_t *kd = reinterpret_cast<uint8_t *>(&sm.k[kb & 1][0][0]) + lane * 16;
+            uint8_t *vd = reinterpret_cast<uint8_t *>(&sm.vt[(kb + 1) & 1][0][0]) + lane * 16;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                *reinterpret_cast<u32x4_t *>(kd + min(static_cast<int>(wv) + 8 * i, kKImg / 1024 - 1) * 1024) = kr[i];
+                *reinterpret_cast<u32x4_t *>(vd + min(static_cast<int>(wv) + 8 * i, kVImg / 1024 - 1) * 1024) = vr[i];
+            }
+        }
+        if constexpr (!(LAB & 16)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (!(LAB & 32)) __syncthreads();
     };
     float16_t sa[2], sb[2];
     qk(sa, sm.k[0]);
@@ -628,7 +670,8 @@ extern "C" int dllm_kv_attention(const void *Q, const uint8_t *Kq, const float *
     dim3 grid(static_cast<unsigned>((S + kQT - 1) / kQT), static_cast<unsigned>(H));
     // DLLM_ATTN_LAB (measurement only; results are garbage when set): 1 no softmax, 2 no K/V
     // staging, 4 no PV MFMAs, 8 no QK MFMAs (on the v4 kernel); 100: the v4 kernel itself (valid
-    // results); 100 + mask: the same masks on the v5 kernel.
+    // results); 100 + mask: the same masks on the v5 kernel, plus 16 no vmcnt wait at the end of a
+    // k-block, 32 no barrier there, 64 register staging instead of LDS-DMA (valid results).
     static const int lab = [] { const char *e = getenv("DLLM_ATTN_LAB"); return e ? atoi(e) : 0; }();
     const _Float16 *Qh = static_cast<const _Float16 *>(Q);
     _Float16 *Oh = static_cast<_Float16 *>(O);
@@ -641,7 +684,8 @@ extern "C" int dllm_kv_attention(const void *Q, const uint8_t *Kq, const float *
             kv_attention_kernel<0><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh);
             break;
 #define DLLM_ALAB5(L) case 100 + L: kv_attention5_kernel<L><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh); break;
-        DLLM_ALAB5(1) DLLM_ALAB5(2) DLLM_ALAB5(4) DLLM_ALAB5(8) DLLM_ALAB5(12) DLLM_ALAB5(13) DLLM_ALAB5(3)
+        DLLM_ALAB5(1) DLLM_ALAB5(2) DLLM_ALAB5(4) DLLM_ALAB5(8) DLLM_ALAB5(12) DLLM_ALAB5(13) DLLM_ALAB5(3) DLLM_ALAB5(16)
+        DLLM_ALAB5(48) DLLM_ALAB5(50) DLLM_ALAB5(64)
 #undef DLLM_ALAB5
         default:
             kv_attention5_kernel<0><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh);

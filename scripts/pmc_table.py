@@ -7,7 +7,7 @@ for d in sys.argv[1:]:
     for f in Path(d).rglob("*counter_collection.csv"):
         for r in csv.DictReader(open(f)):
             kn = r["Kernel_Name"]
-            name = kn[kn.index("::wq") + 2: kn.index(">(") + 1] if "::wq" in kn else kn[:50]
+            name = kn.split("(")[0][:70]
             agg[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for name, cs in agg.items():
     print(name)
