@@ -44,6 +44,7 @@ struct dllm_linear {
     size_t xws_elems = 0;
     int variant = 4;              // prefill schedule variant (tuning knob, see wq_gemm_kernel)
     int dlab = 0;                 // decode-kernel ablation mask (measurement only; 0 in production)
+    int dcfg = 0;                 // decode (NT, nsplit) override (measurement knob; 0 = policy)
     int rlab = 0;                 // ring-kernel ablation mask (measurement only; 0 in production)
     int pplab = 0;                // ping-pong-kernel ablation mask (measurement only; 0 in production)
     std::mutex mu;
@@ -1139,165 +1140,6 @@ wq_gemm16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Decode GEMM (small M, weight-streaming / HBM-bound): one block per 16-column n-tile
-// (N/16 blocks = 256 at N = 4096, one per CU), 8 waves split K by 128-deep slabs, 16x16x32
-// f16 MFMA with the weight as A (16 columns) and MT 16-token tiles of X as B, then the 8 wave
-// partials are summed through LDS (no cross-block reduction, deterministic order).
-// Decode layout: [n16 tile][k128 slab][lane][BITS words], lane l = (n & 15) + 16 * ((k % 32) / 8),
-// word/pair order as the prefill layout with the 32-deep step t in place of the substep.
-// ---------------------------------------------------------------------------------------------
-typedef float float4_t __attribute__((ext_vector_type(4)));
-constexpr int kDecWaves = 8;
-
-template <int BITS, typename YT, int MT, int LAB = 0>
-__global__ void __launch_bounds__(kDecWaves * 64)
-wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdec,
-                 const uint32_t *__restrict__ sz, const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad,
-                 int group) {
-    // Slabs in flight per wave: every load of a round (W words, scales, X fragments) is issued
-    // before the first MFMA, so a round costs one memory latency, not one per 32-deep step.
-    // The load phase has no branch and every loop bound is wave-uniform (scalar wave index): a
-    // per-lane branch around a load makes the compiler wait for it at the join, which serialises
-    // the rounds into one HBM latency per slab.  Rows >= M, steps past K and the clamped duplicate
-    // slabs of the last round read X through a buffer resource with an out-of-range offset, which
-    // returns zeros without a memory access; X is thereby also free of per-lane selects.
-    constexpr int kDepth = MT <= 2 ? 4 : 2;
-    constexpr uint32_t kOOB = 0x80000000u;
-    __shared__ __attribute__((aligned(16))) float red[kDecWaves * MT * 64 * 4];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int n0 = blockIdx.x * 16;
-    const int nslab = (K + 127) / 128;
-    const uint32_t *wbase = wdec + (static_cast<size_t>(blockIdx.x) * nslab * 64 + lane) * BITS;
-    // Scales: one dword per lane per slab, lane l fetching (column l & 15, 32-deep step l >> 4);
-    // step t's value for column c is then pulled from lane c + 16 t.
-    const uint32_t *szcol = sz + n0 + (lane & 15);
-    const int sz_step = lane >> 4;
-    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<__half *>(X), 0, static_cast<int>(static_cast<size_t>(M) * K * 2), 0x00020000);
-    uint32_t xoff[MT];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-        const int m = mt * 16 + (lane & 15);
-        xoff[mt] = m < M ? static_cast<uint32_t>((m * K + 8 * (lane >> 4)) * 2) : kOOB;
-    }
-    // The epilogue's bias is fetched now, behind the weight stream, not after the reduction.
-    const int nb0 = n0 + 4 * (lane >> 4);
-    const float4 bv = *reinterpret_cast<const float4 *>(bias + nb0);
-
-    float4_t acc[MT];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) acc[mt] = float4_t{0.f, 0.f, 0.f, 0.f};
-
-    for (int base = wave; base < nslab; base += kDecWaves * kDepth) {
-        uint32_t w[kDepth][BITS];
-        uint32_t szl[kDepth];
-        half8_t xb[kDepth][4][MT];
-#pragma unroll
-        for (int i = 0; i < kDepth; ++i) {
-            const int slab_raw = base + i * kDecWaves;
-            const int slab = min(slab_raw, nslab - 1);
-            if constexpr (LAB & 4) {
-#pragma unroll
-                for (int j = 0; j < BITS; ++j) w[i][j] = lane * 0x01010101u + j + slab;
-            } else {
-                load_words<BITS>(w[i], wbase + static_cast<size_t>(slab) * 64 * BITS);
-            }
-            const int ks = min(slab * 128 + sz_step * 32, K - 32);
-            if constexpr (LAB & 2) szl[i] = 0x3c00e400u + ks;
-            else szl[i] = szcol[static_cast<size_t>(ks / group) * Npad];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const int k = slab_raw * 128 + t * 32;
-                const bool step_ok = slab_raw < nslab && k < K;
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt) {
-                    if constexpr (LAB & 1) {
-                        xb[i][t][mt] = half8_t{(_Float16)k, 1, 1, 1, 1, 1, 1, (_Float16)lane};
-                    } else {
-                        const uint32_t off = step_ok ? xoff[mt] + static_cast<uint32_t>(k * 2) : kOOB;
-                        xb[i][t][mt] = __builtin_bit_cast(
-                            half8_t, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
-                    }
-                }
-            }
-        }
-        // Keep the scheduler from sinking the loads back next to their MFMAs (it does so to cut
-        // register pressure, which turns the round into one serial latency per fragment).
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < kDepth; ++i) {
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const uint32_t szv = static_cast<uint32_t>(
-                    __builtin_amdgcn_ds_bpermute(((lane & 15) + 16 * t) * 4, static_cast<int>(szl[i])));
-                half2_t nz, sc;
-                split_sz(szv, nz, sc);
-                const half8_t a = dequant_frag<BITS>(w[i], t, nz, sc);
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt)
-                    acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, xb[i][t][mt], acc[mt], 0, 0, 0);
-            }
-        }
-    }
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-        *reinterpret_cast<float4_t *>(red + ((wave * MT + mt) * 64 + lane) * 4) = acc[mt];
-    __syncthreads();
-    // Wave mt (< MT) sums the 8 partials of m-tile mt in wave order (deterministic).
-    for (int mt = wave; mt < MT; mt += kDecWaves) {
-        float4_t s = float4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int w = 0; w < kDecWaves; ++w) s += *reinterpret_cast<const float4_t *>(red + ((w * MT + mt) * 64 + lane) * 4);
-        const int m = mt * 16 + (lane & 15);
-        if (m < M && nb0 < N) {
-            YT *yrow = Y + static_cast<size_t>(m) * N;
-            const float y0 = s[0] + bv.x, y1 = s[1] + bv.y, y2 = s[2] + bv.z, y3 = s[3] + bv.w;
-            if ((N % 4) == 0) {
-                store4<YT>(yrow + nb0, y0, y1, y2, y3);
-            } else {
-                store1<YT>(yrow + nb0, y0);
-                if (nb0 + 1 < N) store1<YT>(yrow + nb0 + 1, y1);
-                if (nb0 + 2 < N) store1<YT>(yrow + nb0 + 2, y2);
-                if (nb0 + 3 < N) store1<YT>(yrow + nb0 + 3, y3);
-            }
-        }
-    }
-}
-
-constexpr int kDecodeMaxM = 64;
-
-template <int BITS, typename YT>
-int launch_decode(const dllm_linear *h, const __half *X, size_t M, YT *Y, hipStream_t st) {
-    const unsigned nb = static_cast<unsigned>(h->Npad / 16);
-    const int Mi = static_cast<int>(M), K = static_cast<int>(h->K), N = static_cast<int>(h->N);
-    const int Np = static_cast<int>(h->Npad), gr = static_cast<int>(h->group);
-    if (M <= 16 && h->dlab != 0) {
-        switch (h->dlab) {
-#define DLLM_DLAB(L) case L: wq_decode_kernel<BITS, YT, 1, L><<<nb, kDecWaves * 64, 0, st>>>(X, Mi, K, h->wdec, h->sz, h->bias, Y, N, Np, gr); break;
-            DLLM_DLAB(1) DLLM_DLAB(2) DLLM_DLAB(3) DLLM_DLAB(4) DLLM_DLAB(5) DLLM_DLAB(6) DLLM_DLAB(7)
-#undef DLLM_DLAB
-            default: break;
-        }
-    } else if (M <= 16)
-        wq_decode_kernel<BITS, YT, 1><<<nb, kDecWaves * 64, 0, st>>>(X, Mi, K, h->wdec, h->sz, h->bias, Y, N, Np, gr);
-    else if (M <= 32)
-        wq_decode_kernel<BITS, YT, 2><<<nb, kDecWaves * 64, 0, st>>>(X, Mi, K, h->wdec, h->sz, h->bias, Y, N, Np, gr);
-    else
-        wq_decode_kernel<BITS, YT, 4><<<nb, kDecWaves * 64, 0, st>>>(X, Mi, K, h->wdec, h->sz, h->bias, Y, N, Np, gr);
-    DLLM_LAUNCH_CHECK();
-    return DLLM_OK;
-}
-
-template <int BITS, typename YT, int VAR>
-void launch_prefill(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t st) {
-    const int nbm = (M + kBM - 1) / kBM, nbn = static_cast<int>(h->Npad / kBN);
-    const unsigned nb = static_cast<unsigned>(nbm) * nbn;
-    wq_gemm_kernel<BITS, YT, VAR><<<nb, kThreads, 0, st>>>(X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N,
-                                                           (int)h->Npad, (int)h->group, nbm, nbn);
-}
-
 // Split-K combine: Y[m][n] = sum_s ws[s][m][n] (slice order) + bias[n]; 4 outputs per thread.
 template <typename YT, int EPI = 0>
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float *__restrict__ ws, int nsplit, int M, int N,
@@ -1323,6 +1165,250 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float *__restr
             store_out4<YT>(Y + static_cast<size_t>(m) * N, bias, n, N, vec_ok, a.x, a.y, a.z, a.w);
         }
     }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Decode GEMM (small M, weight-streaming / HBM-bound): one block per 16 NT-column group and
+// K-slice (grid Npad/(16 NT) x nsplit), 8 waves split the block's K-slice by 128-deep slabs,
+// 16x16x32 f16 MFMA with the weight as A (16 columns per n16 tile) and MT 16-token tiles of X as
+// B, then the 8 wave partials are summed through LDS in wave order.  NT > 1 reuses each X
+// fragment for NT weight tiles: at M = 64 a 16-column block reads 512 KiB of X from L2 for 32 KiB
+// of weight, so the per-CU load path, not HBM, bounded the NT = 1 kernel.  With nsplit > 1 each
+// K-slice writes an f32 slab and splitk_reduce_kernel sums the slabs in slice order (+ bias):
+// deterministic, no atomics.
+// Decode layout: [n16 tile][k128 slab][lane][BITS words], lane l = (n & 15) + 16 * ((k % 32) / 8),
+// word/pair order as the prefill layout with the 32-deep step t in place of the substep.
+// ---------------------------------------------------------------------------------------------
+typedef float float4_t __attribute__((ext_vector_type(4)));
+constexpr int kDecWaves = 8;
+
+template <int BITS, typename YT, int MT, int NT = 1, bool SPLIT = false, int LAB = 0>
+__global__ void __launch_bounds__(kDecWaves * 64)
+wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdec,
+                 const uint32_t *__restrict__ sz, const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad,
+                 int group, int nsplit = 1, float *__restrict__ ws = nullptr) {
+    // Slabs in flight per wave: every load of a round (W words, scales, X fragments) is issued
+    // before the first MFMA, so a round costs one memory latency, not one per 32-deep step.
+    // The load phase has no branch and every loop bound is wave-uniform (scalar wave index): a
+    // per-lane branch around a load makes the compiler wait for it at the join, which serialises
+    // the rounds into one HBM latency per slab.  Rows >= M, steps past K and the clamped duplicate
+    // slabs of the last round read X through a buffer resource with an out-of-range offset, which
+    // returns zeros without a memory access; X is thereby also free of per-lane selects.
+    // Rounds of slabs in flight per wave, sized to the registers one slab's operands take.
+    constexpr int kPerSlab = NT * BITS + NT + 16 * MT;
+    constexpr int kDepth = NT == 1 ? (MT <= 2 ? 4 : 2) : (128 / kPerSlab < 1 ? 1 : (128 / kPerSlab > 4 ? 4 : 128 / kPerSlab));
+    constexpr uint32_t kOOB = 0x80000000u;
+    __shared__ __attribute__((aligned(16))) float red[kDecWaves * MT * NT * 64 * 4];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int n0 = blockIdx.x * 16 * NT;
+    const int nslab = (K + 127) / 128;
+    // this block's K-slice: slabs [s_beg, s_end)
+    const int s_beg = static_cast<int>(static_cast<long>(blockIdx.y) * nslab / nsplit);
+    const int s_end = static_cast<int>(static_cast<long>(blockIdx.y + 1) * nslab / nsplit);
+    const uint32_t *wbase = wdec + (static_cast<size_t>(blockIdx.x) * NT * nslab * 64 + lane) * BITS;
+    const size_t wtile = static_cast<size_t>(nslab) * 64 * BITS;   // words per n16 tile
+    // Scales: one dword per lane per slab and tile, lane l fetching (column l & 15, 32-deep step
+    // l >> 4); step t's value for column c is then pulled from lane c + 16 t.
+    const uint32_t *szcol = sz + n0 + (lane & 15);
+    const int sz_step = lane >> 4;
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<__half *>(X), 0, static_cast<int>(static_cast<size_t>(M) * K * 2), 0x00020000);
+    uint32_t xoff[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        const int m = mt * 16 + (lane & 15);
+        xoff[mt] = m < M ? static_cast<uint32_t>((m * K + 8 * (lane >> 4)) * 2) : kOOB;
+    }
+    // The epilogue's bias is fetched now, behind the weight stream, not after the reduction.
+    float4 bv[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+        bv[nt] = SPLIT ? float4{0.f, 0.f, 0.f, 0.f}
+                       : *reinterpret_cast<const float4 *>(bias + n0 + 16 * nt + 4 * (lane >> 4));
+
+    float4_t acc[NT][MT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = float4_t{0.f, 0.f, 0.f, 0.f};
+
+    for (int base = s_beg + wave; base < s_end; base += kDecWaves * kDepth) {
+        uint32_t w[kDepth][NT][BITS];
+        uint32_t szl[kDepth][NT];
+        half8_t xb[kDepth][4][MT];
+#pragma unroll
+        for (int i = 0; i < kDepth; ++i) {
+            const int slab_raw = base + i * kDecWaves;
+            const int slab = min(slab_raw, s_end - 1);
+            const int ks = min(slab * 128 + sz_step * 32, K - 32);
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                if constexpr (LAB & 4) {
+#pragma unroll
+                    for (int j = 0; j < BITS; ++j) w[i][nt][j] = lane * 0x01010101u + j + slab;
+                } else {
+                    load_words<BITS>(w[i][nt], wbase + nt * wtile + static_cast<size_t>(slab) * 64 * BITS);
+                }
+                if constexpr (LAB & 2) szl[i][nt] = 0x3c00e400u + ks;
+                else szl[i][nt] = szcol[static_cast<size_t>(ks / group) * Npad + 16 * nt];
+            }
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int k = slab_raw * 128 + t * 32;
+                const bool step_ok = slab_raw < s_end && k < K;
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt) {
+                    if constexpr (LAB & 1) {
+                        xb[i][t][mt] = half8_t{(_Float16)k, 1, 1, 1, 1, 1, 1, (_Float16)lane};
+                    } else {
+                        const uint32_t off = step_ok ? xoff[mt] + static_cast<uint32_t>(k * 2) : kOOB;
+                        xb[i][t][mt] = __builtin_bit_cast(
+                            half8_t, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+                    }
+                }
+            }
+        }
+        // Keep the scheduler from sinking the loads back next to their MFMAs (it does so to cut
+        // register pressure, which turns the round into one serial latency per fragment).
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < kDepth; ++i) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) {
+                    const uint32_t szv = static_cast<uint32_t>(
+                        __builtin_amdgcn_ds_bpermute(((lane & 15) + 16 * t) * 4, static_cast<int>(szl[i][nt])));
+                    half2_t nz, sc;
+                    split_sz(szv, nz, sc);
+                    const half8_t a = dequant_frag<BITS>(w[i][nt], t, nz, sc);
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt)
+                        acc[nt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, xb[i][t][mt], acc[nt][mt], 0, 0, 0);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+            *reinterpret_cast<float4_t *>(red + ((wave * MT * NT + nt * MT + mt) * 64 + lane) * 4) = acc[nt][mt];
+    __syncthreads();
+    // Wave j sums the 8 partials of tiles j, j + 8, ... (tile = nt * MT + mt) in wave order.
+    for (int tile = wave; tile < MT * NT; tile += kDecWaves) {
+        float4_t s = float4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int w = 0; w < kDecWaves; ++w)
+            s += *reinterpret_cast<const float4_t *>(red + ((w * MT * NT + tile) * 64 + lane) * 4);
+        const int nt = tile / MT, mt = tile % MT;
+        const int m = mt * 16 + (lane & 15);
+        const int nb0 = n0 + 16 * nt + 4 * (lane >> 4);
+        if constexpr (SPLIT) {
+            // slab [split][M][Npad]; Npad covers every column of the block
+            if (m < M)
+                *reinterpret_cast<float4_t *>(ws + (static_cast<size_t>(blockIdx.y) * M + m) * Npad + nb0) = s;
+        } else if (m < M && nb0 < N) {
+            // bias of this tile: bv[nt] (nt is wave-uniform, select without dynamic indexing)
+            float4 b = bv[0];
+#pragma unroll
+            for (int j = 1; j < NT; ++j)
+                if (nt == j) b = bv[j];
+            YT *yrow = Y + static_cast<size_t>(m) * N;
+            const float y0 = s[0] + b.x, y1 = s[1] + b.y, y2 = s[2] + b.z, y3 = s[3] + b.w;
+            if ((N % 4) == 0) {
+                store4<YT>(yrow + nb0, y0, y1, y2, y3);
+            } else {
+                store1<YT>(yrow + nb0, y0);
+                if (nb0 + 1 < N) store1<YT>(yrow + nb0 + 1, y1);
+                if (nb0 + 2 < N) store1<YT>(yrow + nb0 + 2, y2);
+                if (nb0 + 3 < N) store1<YT>(yrow + nb0 + 3, y3);
+            }
+        }
+    }
+}
+
+constexpr int kDecodeMaxM = 64;
+
+// Decode tile policy: (NT, nsplit) per M bucket, chosen from the M-sweep;
+// h->dcfg (measurement knob) overrides it: dcfg = 16 * log2(NT) + log2(nsplit) + 1.
+// Measured (scripts/decode_sweep.py, 48-layer graph, K = N = 4096 int4, us per layer): the
+// slab combine's extra launch costs ~4.7 us, more than any X saving it buys, and NT = 4 leaves
+// 64 blocks whose per-CU load rate bounds the stream; only M 9..16 gains (NT 2: 7.8 vs 10.2).
+inline void decode_policy(int M, int &nt, int &nsplit) {
+    nsplit = 1;
+    nt = (M > 8 && M <= 16) ? 2 : 1;
+}
+
+template <int BITS, typename YT, int MT, int NT>
+int launch_decode_nt(const dllm_linear *h, const __half *X, int M, YT *Y, int nsplit, hipStream_t st) {
+    const unsigned nbx = static_cast<unsigned>(h->Npad / (16 * NT));
+    const int K = static_cast<int>(h->K), N = static_cast<int>(h->N);
+    const int Np = static_cast<int>(h->Npad), gr = static_cast<int>(h->group);
+    const int nslab = (K + 127) / 128;
+    nsplit = std::max(1, std::min(nsplit, nslab));
+    if (nsplit == 1) {
+        wq_decode_kernel<BITS, YT, MT, NT><<<nbx, kDecWaves * 64, 0, st>>>(X, M, K, h->wdec, h->sz, h->bias, Y, N, Np, gr);
+        DLLM_LAUNCH_CHECK();
+        return DLLM_OK;
+    }
+    float *ws = device_workspace(st, static_cast<size_t>(nsplit) * M * h->Npad * sizeof(float));
+    if (!ws) return DLLM_ERR_HIP;
+    wq_decode_kernel<BITS, YT, MT, NT, true><<<dim3(nbx, static_cast<unsigned>(nsplit)), kDecWaves * 64, 0, st>>>(
+        X, M, K, h->wdec, h->sz, h->bias, Y, N, Np, gr, nsplit, ws);
+    DLLM_LAUNCH_CHECK();
+    const size_t q = static_cast<size_t>(M) * (h->Npad / 4);
+    const unsigned rb = static_cast<unsigned>(std::min<size_t>((q + 255) / 256, 4 * kCUs));
+    splitk_reduce_kernel<YT><<<rb, 256, 0, st>>>(ws, nsplit, M, N, Np, h->bias, Y, PSampleEpi{});
+    DLLM_LAUNCH_CHECK();
+    return DLLM_OK;
+}
+
+template <int BITS, typename YT, int MT>
+int launch_decode_mt(const dllm_linear *h, const __half *X, int M, YT *Y, int nt, int nsplit, hipStream_t st) {
+    switch (nt) {
+    case 2: return launch_decode_nt<BITS, YT, MT, 2>(h, X, M, Y, nsplit, st);
+    case 4: return launch_decode_nt<BITS, YT, MT, 4>(h, X, M, Y, nsplit, st);
+    default: return launch_decode_nt<BITS, YT, MT, 1>(h, X, M, Y, nsplit, st);
+    }
+}
+
+template <int BITS, typename YT>
+int launch_decode(const dllm_linear *h, const __half *X, size_t M, YT *Y, hipStream_t st) {
+    const unsigned nb = static_cast<unsigned>(h->Npad / 16);
+    const int Mi = static_cast<int>(M), K = static_cast<int>(h->K), N = static_cast<int>(h->N);
+    const int Np = static_cast<int>(h->Npad), gr = static_cast<int>(h->group);
+    if (M <= 16 && h->dlab != 0) {
+        switch (h->dlab) {
+#define DLLM_DLAB(L) case L: wq_decode_kernel<BITS, YT, 1, 1, false, L><<<nb, kDecWaves * 64, 0, st>>>(X, Mi, K, h->wdec, h->sz, h->bias, Y, N, Np, gr); break;
+            DLLM_DLAB(1) DLLM_DLAB(2) DLLM_DLAB(3) DLLM_DLAB(4) DLLM_DLAB(5) DLLM_DLAB(6) DLLM_DLAB(7)
+#undef DLLM_DLAB
+            default: break;
+        }
+        DLLM_LAUNCH_CHECK();
+        return DLLM_OK;
+    }
+    int nt, nsplit;
+    if (h->dcfg > 0) {
+        nt = 1 << ((h->dcfg - 1) / 16);
+        nsplit = 1 << ((h->dcfg - 1) % 16);
+    } else {
+        decode_policy(Mi, nt, nsplit);
+    }
+    // the column group must tile Npad (a multiple of 128)
+    while (nt > 1 && h->Npad % (16 * nt)) nt /= 2;
+    if (M <= 16) return launch_decode_mt<BITS, YT, 1>(h, X, Mi, Y, nt, nsplit, st);
+    if (M <= 32) return launch_decode_mt<BITS, YT, 2>(h, X, Mi, Y, nt, nsplit, st);
+    return launch_decode_mt<BITS, YT, 4>(h, X, Mi, Y, nt, nsplit, st);
+}
+
+template <int BITS, typename YT, int VAR>
+void launch_prefill(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t st) {
+    const int nbm = (M + kBM - 1) / kBM, nbn = static_cast<int>(h->Npad / kBN);
+    const unsigned nb = static_cast<unsigned>(nbm) * nbn;
+    wq_gemm_kernel<BITS, YT, VAR><<<nb, kThreads, 0, st>>>(X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N,
+                                                           (int)h->Npad, (int)h->group, nbm, nbn);
 }
 
 // Mid-M prefill (too few 256-row tiles to fill 256 CUs): 128-row tiles, and when even those are
@@ -1692,6 +1778,10 @@ size_t dllm_linear_weight_bytes(dllm_linear_t h) {
 
 int dllm_linear_set_kernel_variant(dllm_linear_t h, int variant) {
     if (!h) return fail(DLLM_ERR_INVALID_PARAMS, "null handle");
+    if (variant >= 200 && variant < 264) {   // decode (NT, nsplit) override (measurement only)
+        h->dcfg = variant - 199;
+        return DLLM_OK;
+    }
     if (variant >= 16 && variant < 24) {   // decode ablation mask (measurement only)
         h->dlab = variant - 16;
         return DLLM_OK;
@@ -1706,9 +1796,9 @@ int dllm_linear_set_kernel_variant(dllm_linear_t h, int variant) {
         return DLLM_OK;
     }
     if (variant < 0 || variant > 11)
-        return fail(DLLM_ERR_INVALID_PARAMS, "variant must be 0..11 (16..23, 32..95, 100..195: ablations)");
+        return fail(DLLM_ERR_INVALID_PARAMS, "variant must be 0..11 (16..23, 32..95, 100..195, 200..263: ablations)");
     h->variant = variant;
-    h->dlab = h->rlab = h->pplab = 0;
+    h->dlab = h->rlab = h->pplab = h->dcfg = 0;
     return DLLM_OK;
 }
 

@@ -445,3 +445,33 @@ def test_gemm_variants_bit_identical(dllm, torch):
         outs[v] = lin(X, out_dtype=torch.float32)
         outs16[v] = lin(X, out_dtype=torch.float16)
     assert torch.equal(outs[8], outs[11]) and torch.equal(outs16[8], outs16[11])
+
+
+@pytest.mark.parametrize("bits", [2, 4, 8])
+def test_linear_decode_tiles_exact_integers(dllm, torch, orc, bits):
+    """Decode kernel (M <= 64) under every (NT column tiles, K-split) configuration on
+    exact-integer data (K = 576: a half 128-deep slab at the end; N = 200: a padded last column
+    group; integer bias): every partial and the ordered slab combine are exact, so each output
+    equals the f64 product bit for bit, for f32 and f16 outputs, at ragged M."""
+    K, N = 576, 200
+    rng = np.random.default_rng(41 + bits)
+    q = (1 << bits) - 1
+    W = rng.integers(0, q + 1, (K, N)).astype(np.float32)
+    for g0 in range(0, K, 128):
+        W[g0, :], W[g0 + 1, :] = 0.0, float(q)
+    b = rng.integers(-4, 5, N).astype(np.float32)
+    lin = dllm.QuantLinear.from_weight(dev(torch, W), dev(torch, b), bits, 128)
+    for M in (1, 5, 16, 17, 33, 64):
+        X = rng.integers(-2, 3, (M, K)).astype(np.float32)
+        ref = (X.astype(np.float64) @ W.astype(np.float64) + b).astype(np.float32)
+        Xd = dev(torch, X).half()
+        for nt_log in (0, 1, 2):
+            for split_log in (0, 1, 2, 3):
+                lin.set_kernel_variant(200 + 16 * nt_log + split_log)
+                Y = host(lin(Xd, out_dtype=torch.float32))
+                assert np.array_equal(Y, ref), (bits, M, 1 << nt_log, 1 << split_log)
+                Y16 = host(lin(Xd, out_dtype=torch.float16).float())
+                assert np.array_equal(Y16, ref.astype(np.float16).astype(np.float32)), (bits, M, nt_log, split_log)
+        lin.set_kernel_variant(4)
+        assert np.array_equal(host(lin(Xd, out_dtype=torch.float32)), ref), (bits, M, "policy")
+    lin.close()
