@@ -400,6 +400,28 @@ def test_kv_attention_peaked_softmax(dllm, torch, orc):
     assert rel_err(O[5], Oref[5]) <= REL_TOL
 
 
+@pytest.mark.parametrize("S,H,bits", [(512, 2, 4), (333, 3, 8), (8192, 2, 4)])
+def test_kv_attention_schedules_bit_identical(dllm, torch, orc, S, H, bits, monkeypatch):
+    """The v5 (DLLM_ATTN_LAB=0) and v6 (4 waves x 64 queries: 200) schedules share the block
+    order and every per-query operation, so their outputs must agree bit for bit, including a
+    ragged last key block and query tile; v4 (100) sums the row in a different order (a chain,
+    not a tree), so it agrees within rounding."""
+    g = torch.Generator(device="cuda").manual_seed(S + H)
+    K = torch.randn(S, H, 128, device="cuda", generator=g)
+    V = torch.randn(S, H, 128, device="cuda", generator=g)
+    Q = torch.randn(S, H, 128, device="cuda", generator=g).half()
+    kq = dllm.QuantizedTensor.quantize(K, bits, packed=True)
+    vq = dllm.QuantizedTensor.quantize(V, bits, packed=True)
+    outs = {}
+    for lab in (0, 100, 200):
+        monkeypatch.setenv("DLLM_ATTN_LAB", str(lab))
+        outs[lab] = dllm.kv_attention(Q, kq, vq)
+    monkeypatch.delenv("DLLM_ATTN_LAB")
+    assert torch.equal(outs[0], outs[200])
+    d4 = (outs[0].float() - outs[100].float()).norm() / outs[100].float().norm()
+    assert d4.item() <= 1e-3, d4.item()
+
+
 # ---- host-slice entry points (the literal Rust signatures) ---------------------------------------
 
 def test_host_entry_points(dllm, orc):
