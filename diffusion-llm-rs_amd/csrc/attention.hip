@@ -614,6 +614,12 @@ kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__
         if constexpr (!(LAB & 16)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if constexpr (!(LAB & 32)) __syncthreads();
     };
+    // LAB & 128 (A/B): static priority 1 for the second-dispatched half (waves 4-7), which
+    // otherwise loses every VALU arbitration to its older SIMD partner (MI355X_MICROARCH.md, two
+    // waves per SIMD, item 4).
+    if constexpr (LAB & 128) {
+        if (wave >= kWaves / 2) __builtin_amdgcn_s_setprio(1);
+    }
     float16_t sa[2], sb[2];
     qk(sa, sm.k[0]);
     for (int kb = 0; kb < nkb; kb += 2) {
@@ -932,7 +938,7 @@ extern "C" int dllm_kv_attention(const void *Q, const uint8_t *Kq, const float *
             break;
 #define DLLM_ALAB5(L) case 100 + L: kv_attention5_kernel<L><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh); break;
         DLLM_ALAB5(1) DLLM_ALAB5(2) DLLM_ALAB5(4) DLLM_ALAB5(8) DLLM_ALAB5(12) DLLM_ALAB5(13) DLLM_ALAB5(3) DLLM_ALAB5(16)
-        DLLM_ALAB5(48) DLLM_ALAB5(50) DLLM_ALAB5(64)
+        DLLM_ALAB5(48) DLLM_ALAB5(50) DLLM_ALAB5(64) DLLM_ALAB5(128)
 #undef DLLM_ALAB5
         case 200:   // v6: 4 waves x 64 queries (A/B)
             kv_attention6_kernel<0><<<grid, kW6 * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh);
