@@ -1489,6 +1489,8 @@ int launch_auto(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t
                 const PSampleEpi *epi = nullptr) {
     const int np = static_cast<int>(h->Npad);
     const int mb256 = (M + 255) / 256, mb128 = (M + 127) / 128;
+    if (h->variant == 12 && np % 256 == 0 && mb128 * (np / 256) >= kCUs)   // 128 x 256 tiles (A/B)
+        return launch_ring<BITS, YT, 8, 4, 1, EPI>(h, X, M, Y, st, 1, epi);
     if (np % 256 == 0 && mb256 * (np / 256) >= kCUs) {
         if (h->variant >= 9 && h->variant <= 11)   // ping-pong schedules (linear_pp.hip)
             return launch_pp_gemm(BITS, std::is_same<YT, float>::value ? 1 : 0, X, M, (int)h->K,
@@ -1795,8 +1797,8 @@ int dllm_linear_set_kernel_variant(dllm_linear_t h, int variant) {
         h->pplab = (variant - 100) % 32;
         return DLLM_OK;
     }
-    if (variant < 0 || variant > 11)
-        return fail(DLLM_ERR_INVALID_PARAMS, "variant must be 0..11 (16..23, 32..95, 100..195, 200..263: ablations)");
+    if (variant < 0 || variant > 12)
+        return fail(DLLM_ERR_INVALID_PARAMS, "variant must be 0..12 (16..23, 32..95, 100..195, 200..263: ablations)");
     h->variant = variant;
     h->dlab = h->rlab = h->pplab = h->dcfg = 0;
     return DLLM_OK;
