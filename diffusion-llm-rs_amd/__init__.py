@@ -21,7 +21,7 @@ from ._lib import (CalibrationRequired, HipError, InvalidParams, QuantizationErr
                    ShapeMismatch, UnsupportedOperation)
 from . import quantization, quant, kvquant, linear, parallel, diffusion, serde
 from .quantization import (AdaptiveQuantizer, QuantizedKVCacheEntry, QuantizedTensor, compression_ratio, dequantize_tensor, kv_attention,
-                           pack, quantize_tensor, unpack)
+                           pack, quantize_tensor, quantize_tensor_pair, unpack)
 from .quant import CalibrationData, DefaultQuantizer, QuantizationParams, QuantizationType, quant_utils
 from .kvquant import BitQuantizer, PrefillKVQuant, SystemConfig, compress_vectors, decompress_vectors
 from .linear import MixedPrecisionStack, QuantLinear
@@ -30,7 +30,7 @@ from .diffusion import (AlphaMode, BetaSchedule, Cumprod, DenoiseLoop, Diffusion
                         p_sample, randn)
 
 __all__ = [
-    "quantize_tensor", "dequantize_tensor", "pack", "unpack", "compression_ratio", "QuantizedTensor",
+    "quantize_tensor", "quantize_tensor_pair", "dequantize_tensor", "pack", "unpack", "compression_ratio", "QuantizedTensor",
     "QuantizedKVCacheEntry", "kv_attention", "QuantizationType", "QuantizationParams", "DefaultQuantizer", "quant_utils",
     "CalibrationData", "BitQuantizer", "PrefillKVQuant", "SystemConfig", "compress_vectors", "decompress_vectors",
     "QuantLinear", "MixedPrecisionStack", "QuantizationError", "InvalidParams", "UnsupportedOperation",

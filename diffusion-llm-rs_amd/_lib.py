@@ -78,6 +78,7 @@ SIGNATURES = {
     "dllm_device_arch": (INT, [INT, C.c_char_p, S]),
     "dllm_quantize_tensor_workspace": (S, [S]),
     "dllm_quantize_tensor": (INT, [P, S, U8, INT, P, P, P, S, P]),
+    "dllm_quantize_tensor_pair": (INT, [P, S, U8, U8, INT, P, P, P, P, P, S, P]),
     "dllm_dequantize_tensor": (INT, [P, S, U8, INT, P, P, INT, P]),
     "dllm_dequantize_tensor_scalar": (INT, [P, S, U8, INT, FL, FL, P, INT, P]),
     "dllm_compression_ratio": (FL, [S, S, U8]),

@@ -180,22 +180,30 @@ __global__ void __launch_bounds__(kBlock) minmax_partial_kernel(const float *__r
     if (threadIdx.x == 0) partials[blockIdx.x] = make_float2(mx, mn);
 }
 
-// Reduces the partials and computes (scale, zp) exactly as quantization.rs:49-56.
+// (scale, zp) from the extremes exactly as quantization.rs:49-56.
+__device__ __forceinline__ void write_params(float mx, float mn, int bits, float *params) {
+    const float q_min = 0.0f;
+    const float q_max = static_cast<float>(1u << bits) - 1.0f;     // :50
+    float scale = (mx - mn) / (q_max - q_min);                      // :52
+    if (scale == 0.0f) scale = 1.0f;                                // :53
+    const float zpf = q_min - mn / scale;                           // :55
+    const uint32_t zp = rs_as_u8(roundf(rs_clamp(zpf, q_min, q_max)));  // :56
+    params[0] = scale;
+    params[1] = static_cast<float>(zp);                             // :67
+}
+
+// Reduces the partials and writes the params of width `bits` (and of `bits_b` when nonzero:
+// the extremes do not depend on the width).
 __global__ void __launch_bounds__(kBlock) quant_params_kernel(const float2 *__restrict__ partials, int np, int bits,
-                                                              float *__restrict__ params) {
+                                                              float *__restrict__ params, int bits_b = 0,
+                                                              float *__restrict__ params_b = nullptr) {
     __shared__ float smem[2 * kBlock / 64];
     float mx = -INFINITY, mn = INFINITY;
     for (int i = threadIdx.x; i < np; i += kBlock) { float2 p = partials[i]; mx = fmaxf(mx, p.x); mn = fminf(mn, p.y); }
     block_minmax(mx, mn, smem);
     if (threadIdx.x == 0) {
-        const float q_min = 0.0f;
-        const float q_max = static_cast<float>(1u << bits) - 1.0f;     // :50
-        float scale = (mx - mn) / (q_max - q_min);                      // :52
-        if (scale == 0.0f) scale = 1.0f;                                // :53
-        const float zpf = q_min - mn / scale;                           // :55
-        const uint32_t zp = rs_as_u8(roundf(rs_clamp(zpf, q_min, q_max)));  // :56
-        params[0] = scale;
-        params[1] = static_cast<float>(zp);                             // :67
+        write_params(mx, mn, bits, params);
+        if (bits_b) write_params(mx, mn, bits_b, params_b);
     }
 }
 
@@ -221,6 +229,33 @@ __global__ void __launch_bounds__(kBlock) quantize_tensor_kernel(const float *__
             c[i] = (i < cnt) ? rs_round_i32_clamp(t, hi) : 0u;
         }
         store_codes(out, o, cnt, c, bits, packed, vec_out);
+    }
+}
+
+// K2 at two widths of the same x: one read, two code sets (each width's arithmetic exactly K2's).
+__global__ void __launch_bounds__(kBlock) quantize_pair_kernel(const float *__restrict__ x, size_t n, int bits_a,
+                                                               int bits_b, int packed, uint8_t *__restrict__ out_a,
+                                                               uint8_t *__restrict__ out_b,
+                                                               const float *__restrict__ params_a,
+                                                               const float *__restrict__ params_b, int vec_in,
+                                                               int vec_out_a, int vec_out_b) {
+    const float sa = params_a[0], za = params_a[1], sb = params_b[0], zb = params_b[1];
+    const int ha = (1 << bits_a) - 1, hb = (1 << bits_b) - 1;
+    const size_t noct = (n + 7) / 8;
+    for (size_t o = blockIdx.x * static_cast<size_t>(kBlock) + threadIdx.x; o < noct;
+         o += static_cast<size_t>(gridDim.x) * kBlock) {
+        const int cnt = octet_count(o, n);
+        F8 v = load_octet(x, o, cnt, vec_in);
+        uint32_t ca[8], cb[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float ta = v.v[i] / sa + za;
+            const float tb = v.v[i] / sb + zb;
+            ca[i] = (i < cnt) ? rs_round_i32_clamp(ta, ha) : 0u;
+            cb[i] = (i < cnt) ? rs_round_i32_clamp(tb, hb) : 0u;
+        }
+        store_codes(out_a, o, cnt, ca, bits_a, packed, vec_out_a);
+        store_codes(out_b, o, cnt, cb, bits_b, packed, vec_out_b);
     }
 }
 
@@ -541,6 +576,33 @@ int dllm_quantize_tensor(const float *x, size_t n, uint8_t bits, int packed, uin
     if (n) {
         quantize_tensor_kernel<<<octet_grid(n), kBlock, 0, st>>>(x, n, bits, packed, out, params_out,
                                                                  aligned(x, 16), aligned(out, 8));
+        DLLM_LAUNCH_CHECK();
+    }
+    return DLLM_OK;
+}
+
+int dllm_quantize_tensor_pair(const float *x, size_t n, uint8_t bits_a, uint8_t bits_b, int packed, uint8_t *out_a,
+                              float *params_a, uint8_t *out_b, float *params_b, void *workspace,
+                              size_t workspace_bytes, dllm_stream_t stream) {
+    if (bits_a < 1 || bits_a > 8 || bits_b < 1 || bits_b > 8)
+        return fail(DLLM_ERR_INVALID_PARAMS, "Bits must be between 1 and 8");
+    if (!params_a || !params_b || (n && (!x || !out_a || !out_b))) return fail(DLLM_ERR_INVALID_PARAMS, "null pointer");
+    const unsigned nblk = minmax_blocks(n);
+    if (!workspace || workspace_bytes < sizeof(float2) * nblk)
+        return fail(DLLM_ERR_INVALID_PARAMS, "workspace too small (see dllm_quantize_tensor_workspace)");
+    hipStream_t st = as_stream(stream);
+    float2 *partials = static_cast<float2 *>(workspace);
+    if (n) {
+        int rc = launch_minmax(x, n, partials, nblk, st);
+        if (rc) return rc;
+    }
+    quant_params_kernel<<<1, kBlock, 0, st>>>(partials, n ? static_cast<int>(nblk) : 0, bits_a, params_a, bits_b,
+                                              params_b);
+    DLLM_LAUNCH_CHECK();
+    if (n) {
+        quantize_pair_kernel<<<octet_grid(n), kBlock, 0, st>>>(x, n, bits_a, bits_b, packed, out_a, out_b, params_a,
+                                                               params_b, aligned(x, 16), aligned(out_a, 8),
+                                                               aligned(out_b, 8));
         DLLM_LAUNCH_CHECK();
     }
     return DLLM_OK;

@@ -211,6 +211,11 @@ class KVCacheEntry:
         """lib.rs:241-276 (the missing QuantizedKVCacheEntry::update is a re-quantization)."""
         self.keys, self.values = new_keys, new_values
         self.seq_len = int(new_keys.shape[1])
+        if self.prefill_quant_bits > 0 and self.decode_quant_bits > 0:
+            # both widths from one min/max pass and one read per tensor (bit-identical)
+            self.prefill_quantized, self.decode_quantized = QuantizedKVCacheEntry.new_pair(
+                new_keys, new_values, self.prefill_quant_bits, self.decode_quant_bits)
+            return
         if self.prefill_quant_bits > 0:
             self.prefill_quantized = QuantizedKVCacheEntry.new(new_keys, new_values, self.prefill_quant_bits)
         if self.decode_quant_bits > 0:

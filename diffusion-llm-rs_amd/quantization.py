@@ -61,6 +61,27 @@ def quantize_tensor(data: torch.Tensor, bits: int, packed: bool = False):
     return out, params
 
 
+def quantize_tensor_pair(data: torch.Tensor, bits_a: int, bits_b: int, packed: bool = False):
+    """:func:`quantize_tensor` of the same data at two widths in one min/max pass and one read
+    (KVCacheEntry::update's prefill and decode copies, diffuse-llm-rs/src/lib.rs:241-276).
+    Returns ``((codes_a, params_a), (codes_b, params_b))``, bit-identical to two calls."""
+    for b in (bits_a, bits_b):
+        if not 1 <= int(b) <= 8:
+            raise _lib.InvalidParams("Bits must be between 1 and 8")
+    x = _dev(data, torch.float32).reshape(-1)
+    n = x.numel()
+    outs = [torch.empty(packed_bytes(n, b) if packed else n, dtype=torch.uint8, device=x.device)
+            for b in (bits_a, bits_b)]
+    params = [torch.empty(2, dtype=torch.float32, device=x.device) for _ in range(2)]
+    L = _lib.load()
+    ws = torch.empty(max(L.dllm_quantize_tensor_workspace(n), 16), dtype=torch.uint8, device=x.device)
+    ptr = lambda t: _ptr(t) if t.numel() else None  # noqa: E731
+    check(L.dllm_quantize_tensor_pair(_ptr(x) if n else None, n, bits_a, bits_b, int(packed), ptr(outs[0]),
+                                      _ptr(params[0]), ptr(outs[1]), _ptr(params[1]), _ptr(ws), ws.numel(),
+                                      _stream()))
+    return (outs[0], params[0]), (outs[1], params[1])
+
+
 def dequantize_tensor(codes: torch.Tensor, scale, zero_point=None, *, bits: int = 8, packed: bool = False,
                       n: int | None = None, out_dtype=torch.float32) -> torch.Tensor:
     """quantization.rs:81-85 ``dequantize_tensor(data, scale, zero_point)``.
@@ -173,6 +194,17 @@ class QuantizedKVCacheEntry:
         k = QuantizedTensor.quantize(keys, bits, packed)
         v = QuantizedTensor.quantize(values, bits, packed)
         return cls(k, v, int(keys.shape[1]) if keys.dim() > 1 else 0)
+
+    @classmethod
+    def new_pair(cls, keys: torch.Tensor, values: torch.Tensor, bits_a: int, bits_b: int, packed: bool = True):
+        """``new(keys, values, bits_a)`` and ``new(keys, values, bits_b)`` in one pass per tensor
+        (:func:`quantize_tensor_pair`); bit-identical to the two separate calls."""
+        seq = int(keys.shape[1]) if keys.dim() > 1 else 0
+        (ka, pka), (kb, pkb) = quantize_tensor_pair(keys, bits_a, bits_b, packed)
+        (va, pva), (vb, pvb) = quantize_tensor_pair(values, bits_a, bits_b, packed)
+        ks, vs = tuple(keys.shape), tuple(values.shape)
+        return (cls(QuantizedTensor(ka, ks, pka, int(bits_a), packed), QuantizedTensor(va, vs, pva, int(bits_a), packed), seq),
+                cls(QuantizedTensor(kb, ks, pkb, int(bits_b), packed), QuantizedTensor(vb, vs, pvb, int(bits_b), packed), seq))
 
     def dequantize_keys(self, out_dtype=torch.float32) -> torch.Tensor:
         """quantization.rs:160-166."""

@@ -72,6 +72,15 @@ size_t dllm_quantize_tensor_workspace(size_t n);
 int dllm_quantize_tensor(const float *x, size_t n, uint8_t bits, int packed, uint8_t *out, float *params_out,
                          void *workspace, size_t workspace_bytes, dllm_stream_t stream);
 
+/* quantize_tensor of the SAME data at two widths, as KVCacheEntry::update does for its prefill and
+ * decode copies (diffuse-llm-rs/src/lib.rs:241-276, QuantizedKVCacheEntry::new at each width,
+ * quantization.rs:140-157): one min/max pass (the extremes do not depend on the width) and one read
+ * of x that writes both code sets.  Outputs are bit-identical to two dllm_quantize_tensor calls.
+ * Workspace: dllm_quantize_tensor_workspace(n).  bits_a, bits_b in 1..=8. */
+int dllm_quantize_tensor_pair(const float *x, size_t n, uint8_t bits_a, uint8_t bits_b, int packed, uint8_t *out_a,
+                              float *params_a, uint8_t *out_b, float *params_b, void *workspace,
+                              size_t workspace_bytes, dllm_stream_t stream);
+
 /* dequantize_tensor(data: &[u8], scale: f32, zero_point: f32) -> Vec<f32> (quantization.rs:81-85)
  * and QuantizedTensor::dequantize (:115-117):  y = ((q as f32) - zp) * scale.
  * params[2] = {scale, zp} in DEVICE memory (as written by dllm_quantize_tensor).

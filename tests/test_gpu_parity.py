@@ -82,6 +82,26 @@ def test_quantize_tensor_random_sizes(dllm, torch, orc):
                         assert same_bits(host(y), ref.astype(np.float16))
 
 
+@pytest.mark.parametrize("n", [1, 7, 8, 1000, 65537, 1 << 21])
+def test_quantize_tensor_pair_matches_two_calls(dllm, torch, orc, n):
+    """dllm_quantize_tensor_pair (one min/max pass, one read, two widths) == two quantize_tensor
+    calls bit for bit (codes, packed bytes and params), at ragged n and an unaligned base."""
+    rng = np.random.default_rng(n)
+    x = (rng.standard_normal(n + 1) * 3 + 0.5).astype(np.float32)
+    xd = dev(torch, x)[1:]                       # 4-byte but not 16-byte aligned base
+    for packed in (True, False):
+        for ba, bb in ((8, 4), (4, 2), (3, 5), (1, 8)):
+            (ca, pa), (cb, pb) = dllm.quantize_tensor_pair(xd, ba, bb, packed=packed)
+            ra, qa = dllm.quantize_tensor(xd, ba, packed=packed)
+            rb, qb = dllm.quantize_tensor(xd, bb, packed=packed)
+            assert torch.equal(ca, ra) and torch.equal(cb, rb), (n, packed, ba, bb)
+            assert same_bits(host(pa), host(qa)) and same_bits(host(pb), host(qb)), (n, packed, ba, bb)
+    q, s, z = orc.quantize_tensor(x[1:], 4)
+    (c4, p4), _ = dllm.quantize_tensor_pair(xd, 4, 2, packed=True)
+    assert np.array_equal(host(c4), orc.pack_bits(q, 4))
+    assert same_bits(host(p4), np.array([s, z], np.float32))
+
+
 def test_dequantize_scalar_signature(dllm, torch, orc):
     rng = np.random.default_rng(1)
     q = rng.integers(0, 16, 777).astype(np.uint8)
