@@ -1333,12 +1333,13 @@ constexpr int kDecodeMaxM = 64;
 
 // Decode tile policy: (NT, nsplit) per M bucket, chosen from the M-sweep;
 // h->dcfg (measurement knob) overrides it: dcfg = 16 * log2(NT) + log2(nsplit) + 1.
-// Measured (scripts/decode_sweep.py, 48-layer graph, K = N = 4096 int4, us per layer): the
-// slab combine's extra launch costs ~4.7 us, more than any X saving it buys, and NT = 4 leaves
-// 64 blocks whose per-CU load rate bounds the stream; only M 9..16 gains (NT 2: 7.8 vs 10.2).
+// Measured (scripts/decode_sweep.py, 48-layer graph, K = N = 4096 int4, us per layer;
+// profiles/r01_decode_tiles): up to M = 32 the one-tile kernel wins (M 1/16/32: 5.1/6.9/10.7;
+// the slab combine's extra launch costs ~4.7 us and NT = 4 without a split leaves 64 blocks whose
+// per-CU load rate bounds the stream); at M 33..64 X re-reads dominate and NT 4 x 4 K-slices
+// wins (M 64: 13.8 vs 18.6).
 inline void decode_policy(int M, int &nt, int &nsplit) {
-    nsplit = 1;
-    nt = (M > 8 && M <= 16) ? 2 : 1;
+    nt = nsplit = M > 32 ? 4 : 1;
 }
 
 template <int BITS, typename YT, int MT, int NT>
