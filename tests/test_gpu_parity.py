@@ -420,6 +420,28 @@ def test_kv_attention_peaked_softmax(dllm, torch, orc):
     assert rel_err(O[5], Oref[5]) <= REL_TOL
 
 
+def test_kv_quantize_attention_config4_full_size(dllm, torch, orc):
+    """Config C4 at its full size (K, V, Q [8192, 32, 128]): the int4 per-tensor KV quantization
+    is bit-exact against the C oracle on all 33.5 M elements of each tensor (packed codes and
+    params), and the dequant-attention of the first 64 queries of every head (all 8192 keys)
+    is within REL_TOL of the oracle's f64 SDPA on the oracle-dequantized K and V."""
+    S, H, D, rows = 8192, 32, 128, 64
+    rng = np.random.default_rng(84)
+    K = rng.standard_normal((S, H, D), dtype=np.float32)
+    V = rng.standard_normal((S, H, D), dtype=np.float32)
+    Q = rng.standard_normal((S, H, D), dtype=np.float32).astype(np.float16)
+    e = dllm.QuantizedKVCacheEntry.new(dev(torch, K), dev(torch, V), 4)
+    deq = []
+    for t, ref in ((e.keys, K), (e.values, V)):
+        rq, rs, rz = orc.quantize_tensor(ref.ravel(), 4)
+        assert np.array_equal(host(t.data), orc.pack_bits(rq, 4))
+        assert same_bits(host(t.params), np.array([rs, rz], np.float32))
+        deq.append(orc.dequantize_tensor(rq, rs, rz).reshape(S, H, D))
+    O = host(dllm.kv_attention(dev(torch, Q), e.keys, e.values)[:rows].float())
+    Oref = orc.attention(Q.astype(np.float32), deq[0], deq[1], q_rows=rows)
+    assert rel_err(O, Oref) <= REL_TOL, rel_err(O, Oref)
+
+
 @pytest.mark.parametrize("S,H,bits", [(512, 2, 4), (333, 3, 8), (8192, 2, 4)])
 def test_kv_attention_schedules_bit_identical(dllm, torch, orc, S, H, bits, monkeypatch):
     """The v5 (DLLM_ATTN_LAB=0) and v6 (4 waves x 64 queries: 200) schedules share the block
