@@ -381,6 +381,30 @@ def test_mixed_precision_stack(dllm, torch, orc):
     assert torch.equal(stack(x), h)
 
 
+def test_mixed_precision_stack_config3_full_size(dllm, torch, orc):
+    """Config C3 at its full size: 12 layers d = 4096 cycling int2 / int4 on seq 4096.  Each
+    layer's output is within REL_TOL of torch fp32 applied to the same f16 input with the weights
+    the oracle dequantizes from the layer's exported codes; the stack's own forward equals the
+    layer-by-layer chain bit for bit."""
+    d, M, L = 4096, 4096, 12
+    g = torch.Generator(device="cuda").manual_seed(3)
+    stack = dllm.MixedPrecisionStack([0.02 * torch.randn(d, d, device="cuda", generator=g) for _ in range(L)],
+                                     bits=(2, 4))
+    x = torch.randn(M, d, device="cuda", generator=g).half()
+    h = x
+    for i, layer in enumerate(stack.layers):
+        assert layer.bits == (2, 4)[i % 2]
+        y = layer(h, out_dtype=torch.float16)
+        codes, scales, zps = layer.export()
+        Wh = dev(torch, orc.dequantize_weights(orc.unpack_bits(host(codes), d * d, layer.bits).reshape(d, d),
+                                               host(scales), host(zps), 128))
+        yr = h.float() @ Wh
+        rel = (torch.linalg.norm(y.float() - yr) / torch.linalg.norm(yr)).item()
+        assert rel <= REL_TOL, (i, layer.bits, rel)
+        h = y
+    assert torch.equal(stack(x), h)
+
+
 # ---- a9: quantized-KV dequant-attention ---------------------------------------------------------
 
 @pytest.mark.parametrize("S,H,bits", [(256, 2, 4), (200, 3, 4), (96, 1, 8), (512, 4, 4), (33, 2, 4)])
