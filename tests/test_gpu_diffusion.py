@@ -198,3 +198,49 @@ def test_denoise_loop_overlap_bit_identical(dllm, cuda):
     torch.cuda.synchronize()
     assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
     assert torch.equal(kvs[0], kvs[1])
+
+
+def test_denoise_loop_config5_full_size(dllm, cuda, orc):
+    """Config C5 at its full size on one GPU: 12 int4 layers d = 4096, seq 2048, 50 steps with the
+    phase-aware KV cache (8 / 4 bits, progressive) updated every step on the side stream and
+    p_sample fused into the last layer.  Reference: the same recursion in torch f32 on the
+    oracle-dequantized weights with f16 activations between layers, and the noise stream (checked
+    bit-exact against the oracle in test_randn_bit_exact).  Weights 0.5/sqrt(d) N(0,1) keep the
+    state finite over the 50 steps; tolerance 2e-3 relative on the final state.  The KV cache
+    ends in the state of its last update (bit-exact against the oracle)."""
+    import torch
+    d, M, L, steps, seed = 4096, 2048, 12, 50, 5
+    g = torch.Generator(device="cuda").manual_seed(5)
+    layers = [dllm.QuantLinear.from_weight((0.5 / 64.0) * torch.randn(d, d, device="cuda", generator=g), None, 4, 128)
+              for _ in range(L)]
+    cfg = dllm.DiffusionConfig(num_timesteps=steps, hidden_size=d, num_layers=L)
+    K = torch.randn(1, M, d, device="cuda", generator=g)
+    V = torch.randn(1, M, d, device="cuda", generator=g)
+    kv = dllm.KVCacheEntry.new(K, V, cfg.prefill_bits, cfg.decode_bits)
+    loop = dllm.DenoiseLoop(layers, cfg, cumprod=dllm.Cumprod.INCLUSIVE, seed=seed, kv_cache=kv)
+    x0 = torch.randn(M, d, device="cuda", generator=g)
+    out = loop.sample(x0.clone(), steps)
+    assert bool(torch.isfinite(out).all())
+    Wh = []
+    for lin in layers:
+        codes, s, z = lin.export()
+        cd = orc.unpack_bits(codes.cpu().numpy(), d * d, 4).reshape(d, d)
+        Wh.append(torch.from_numpy(orc.dequantize_weights(cd, s.cpu().numpy(), z.cpu().numpy(), 128)).cuda())
+    x = x0.clone()
+    for i, t in enumerate(range(steps - 1, -1, -1)):
+        h = x
+        for j, W in enumerate(Wh):
+            h = h.half().float() @ W
+            if j < L - 1:
+                h = h.half().float()
+        coef, flag = dllm.diffusion.p_sample_coeffs(cfg, [t], 1, dllm.Cumprod.INCLUSIVE)
+        c1, c2, sd = (float(v) for v in coef[0])
+        nz = dllm.randn(M * d, seed, i * M * d).reshape(M, d) if flag else 0.0
+        x = (c1 * x + c2 * h) + sd * nz
+    rel = (torch.linalg.norm(out - x) / torch.linalg.norm(x)).item()
+    assert rel <= 2e-3, rel
+    # the cache's current (decode-phase) copy is the last re-quantization of the pass-through K
+    Kn = K.cpu().numpy().ravel()
+    q, sc, zp = orc.quantize_tensor(Kn, kv.decode_quant_bits)
+    assert np.array_equal(kv.get_keys().cpu().numpy().ravel().view(np.uint32),
+                          orc.dequantize_tensor(q, sc, zp).view(np.uint32))
