@@ -89,6 +89,9 @@ SIGNATURES = {
     "dllm_default_dequantize": (INT, [P, S, FL, I32, P, P]),
     "dllm_calib_update": (INT, [P, S, P, P, S, P, S, P]),
     "dllm_calib_compute_params": (INT, [FL, FL, S, U8, INT, P, P]),
+    "dllm_tensor_extremes": (INT, [P, S, P, P, S, P]),
+    "dllm_quantize_params_from_extremes": (INT, [P, U8, P, P]),
+    "dllm_quantize_tensor_with_params": (INT, [P, S, U8, INT, P, P, P]),
     "dllm_adaptive_update": (INT, [P, S, P, P, S, P]),
     "dllm_adaptive_compute_params": (INT, [P, INT, U32, P, P]),
     "dllm_adaptive_quantize": (INT, [P, S, U32, P, INT, P, P]),

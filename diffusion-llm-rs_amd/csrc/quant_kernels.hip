@@ -192,6 +192,11 @@ __device__ __forceinline__ void write_params(float mx, float mn, int bits, float
     params[1] = static_cast<float>(zp);                             // :67
 }
 
+// Params of width `bits` from caller-held extremes stats[2] = {min, max} (sharded quantize_tensor).
+__global__ void params_from_extremes_kernel(const float *__restrict__ stats, int bits, float *__restrict__ params) {
+    if (threadIdx.x == 0) write_params(stats[1], stats[0], bits, params);
+}
+
 // Reduces the partials and writes the params of width `bits` (and of `bits_b` when nonzero:
 // the extremes do not depend on the width).
 __global__ void __launch_bounds__(kBlock) quant_params_kernel(const float2 *__restrict__ partials, int np, int bits,
@@ -870,6 +875,28 @@ int dllm_decompress_vectors(const uint8_t *q, size_t rows, size_t dim, const flo
         q, rows, dim, scales, zps, out);
     DLLM_LAUNCH_CHECK();
     return DLLM_OK;
+}
+
+// ---- quantize_tensor split at its reduction (a tensor sharded over ranks) -------
+int dllm_tensor_extremes(const float *x, size_t n, float *stats, void *workspace, size_t workspace_bytes,
+                         dllm_stream_t stream) {
+    // The fold of quantization.rs:41-46 (NaN-ignoring max/min), into caller-seeded stats.
+    return dllm_adaptive_update(x, n, stats, workspace, workspace_bytes, stream);
+}
+
+int dllm_quantize_params_from_extremes(const float *stats, uint8_t bits, float *params, dllm_stream_t stream) {
+    if (bits < 1 || bits > 8) return fail(DLLM_ERR_INVALID_PARAMS, "Bits must be between 1 and 8");
+    if (!stats || !params) return fail(DLLM_ERR_INVALID_PARAMS, "null pointer");
+    params_from_extremes_kernel<<<1, 64, 0, as_stream(stream)>>>(stats, bits, params);
+    DLLM_LAUNCH_CHECK();
+    return DLLM_OK;
+}
+
+int dllm_quantize_tensor_with_params(const float *x, size_t n, uint8_t bits, int packed, const float *params,
+                                     uint8_t *out, dllm_stream_t stream) {
+    if (bits < 1 || bits > 8) return fail(DLLM_ERR_INVALID_PARAMS, "Bits must be between 1 and 8");
+    // quantization.rs:61-64 with the params of :49-56 (== the adaptive map for 1 <= bits <= 8).
+    return dllm_adaptive_quantize(x, n, bits, params, packed, out, stream);
 }
 
 }  // extern "C"

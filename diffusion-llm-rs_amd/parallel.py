@@ -141,3 +141,87 @@ class TokenParallelLinear:
         return self.local(x_local, out_dtype=out_dtype)
 
     __call__ = forward
+
+
+def head_range(H: int, world: int, rank: int):
+    """Contiguous head shard [h0, h1) (heads are independent in attention)."""
+    per, rem = divmod(H, world)
+    h0 = rank * per + min(rank, rem)
+    return h0, h0 + per + (1 if rank < rem else 0)
+
+
+class DeviceKVOps:
+    """The per-shard device steps of :class:`HeadParallelKVCache` (HIP kernels behind the C-ABI)."""
+
+    @staticmethod
+    def extremes(x):
+        from .quantization import tensor_extremes
+        return tensor_extremes(x)
+
+    @staticmethod
+    def params(stats, bits):
+        from .quantization import quantize_params_from_extremes
+        return quantize_params_from_extremes(stats, bits)
+
+    @staticmethod
+    def quantize(x, bits, params):
+        from .quantization import quantize_tensor_with_params
+        return quantize_tensor_with_params(x, bits, params, packed=True)
+
+    @staticmethod
+    def attention(q, k, v):
+        from .quantization import kv_attention
+        return kv_attention(q, k, v)
+
+
+class HeadParallelKVCache:
+    """``QuantizedKVCacheEntry`` (diffuse-llm-rs/src/quantization.rs:140-175) with K and V sharded
+    by head over the ranks: rank r holds heads [h0, h1) of K, V, Q ``[S, H, D]`` as
+    its own contiguous ``[S, h1-h0, D]`` tensors.
+
+    The reference quantizes K and V per WHOLE tensor (one scale / zero point each, :142-150), so
+    the shards need the global extremes: each rank folds its shard (NaN-ignoring min/max, the
+    order-independent reduction of :41-46), one ``all_reduce(MAX)`` of 4 floats {-min_K, max_K,
+    -min_V, max_V} combines K and V, and every rank writes the params and codes the unsharded
+    ``quantize_tensor`` writes for its elements -- bit for bit.  Attention is per head, so it runs
+    on the local heads with no exchange.  ``ops`` is pluggable (``DeviceKVOps`` on the GPU; the CPU
+    gloo tests pass the oracle's restatement)."""
+
+    def __init__(self, H: int, bits: int = 4, pg=None, ops=DeviceKVOps):
+        self.pg, self.bits, self.ops = pg, int(bits), ops
+        self.world, self.rank = _world(pg)
+        self.H = H
+        self.h0, self.h1 = head_range(H, self.world, self.rank)
+
+    def local_extremes(self, keys_local: torch.Tensor, values_local: torch.Tensor) -> torch.Tensor:
+        """This rank's {-min_K, max_K, -min_V, max_V} (the all-reduce operand; NaN skipped)."""
+        sk, sv = self.ops.extremes(keys_local), self.ops.extremes(values_local)
+        return torch.stack([-sk[0], sk[1], -sv[0], sv[1]]).contiguous()
+
+    def quantize_with_extremes(self, keys_local: torch.Tensor, values_local: torch.Tensor, red: torch.Tensor):
+        """Params and local codes from the all-reduced extremes ``red``."""
+        kp = self.ops.params(torch.stack([-red[0], red[1]]), self.bits)
+        vp = self.ops.params(torch.stack([-red[2], red[3]]), self.bits)
+        return (self.ops.quantize(keys_local, self.bits, kp), kp, self.ops.quantize(values_local, self.bits, vp), vp)
+
+    def quantize(self, keys_local: torch.Tensor, values_local: torch.Tensor):
+        """QuantizedKVCacheEntry::new(keys, values, bits) on the local heads (global per-tensor params).
+        Returns ``(k_codes, k_params, v_codes, v_params)``: packed local codes, device params."""
+        red = self.local_extremes(keys_local, values_local)
+        if self.world > 1:
+            dist.all_reduce(red, op=dist.ReduceOp.MAX, group=self.pg)
+        return self.quantize_with_extremes(keys_local, values_local, red)
+
+    def entry(self, keys_local: torch.Tensor, values_local: torch.Tensor, red: Optional[torch.Tensor] = None):
+        """The local shard as a ``QuantizedKVCacheEntry``; ``red`` = already all-reduced extremes."""
+        from .quantization import QuantizedKVCacheEntry, QuantizedTensor
+        kc, kp, vc, vp = (self.quantize(keys_local, values_local) if red is None
+                          else self.quantize_with_extremes(keys_local, values_local, red))
+        ks, vs = tuple(keys_local.shape), tuple(values_local.shape)
+        seq = int(keys_local.shape[0]) if keys_local.dim() == 3 else 0
+        return QuantizedKVCacheEntry(QuantizedTensor(kc, ks, kp, self.bits, True),
+                                     QuantizedTensor(vc, vs, vp, self.bits, True), seq)
+
+    def attention(self, q_local: torch.Tensor, entry) -> torch.Tensor:
+        """Dequant-attention of the local heads: O[:, h0:h1, :] of the unsharded call."""
+        return self.ops.attention(q_local, entry.keys, entry.values)

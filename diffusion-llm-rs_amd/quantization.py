@@ -82,6 +82,45 @@ def quantize_tensor_pair(data: torch.Tensor, bits_a: int, bits_b: int, packed: b
     return (outs[0], params[0]), (outs[1], params[1])
 
 
+def tensor_extremes(data: torch.Tensor, stats: torch.Tensor | None = None) -> torch.Tensor:
+    """The extremes fold of quantization.rs:41-46 (NaN-ignoring) as a device f32[2] {min, max},
+    folded into ``stats`` when given (seed {+inf, -inf}).  First half of :func:`quantize_tensor`
+    split at its reduction, for tensors sharded over ranks (``parallel.HeadParallelKVCache``)."""
+    x = _dev(data, torch.float32).reshape(-1)
+    if stats is None:
+        stats = torch.tensor([math.inf, -math.inf], dtype=torch.float32, device=x.device)
+    n = x.numel()
+    if n:
+        L = _lib.load()
+        ws = torch.empty(max(L.dllm_quantize_tensor_workspace(n), 16), dtype=torch.uint8, device=x.device)
+        check(L.dllm_tensor_extremes(_ptr(x), n, _ptr(stats), _ptr(ws), ws.numel(), _stream()))
+    return stats
+
+
+def quantize_params_from_extremes(stats: torch.Tensor, bits: int) -> torch.Tensor:
+    """quantization.rs:49-56: device params {scale, zero_point} from device extremes {min, max}."""
+    if not 1 <= int(bits) <= 8:
+        raise _lib.InvalidParams("Bits must be between 1 and 8")
+    st = _dev(stats, torch.float32)
+    params = torch.empty(2, dtype=torch.float32, device=st.device)
+    check(_lib.load().dllm_quantize_params_from_extremes(_ptr(st), bits, _ptr(params), _stream()))
+    return params
+
+
+def quantize_tensor_with_params(data: torch.Tensor, bits: int, params: torch.Tensor, packed: bool = False):
+    """quantization.rs:59-65 with given device params: the codes :func:`quantize_tensor` writes once
+    the params are known.  Returns the codes (one per byte, or the packed bitstream)."""
+    if not 1 <= int(bits) <= 8:
+        raise _lib.InvalidParams("Bits must be between 1 and 8")
+    x = _dev(data, torch.float32).reshape(-1)
+    n = x.numel()
+    pr = _dev(params, torch.float32)
+    out = torch.empty(packed_bytes(n, bits) if packed else n, dtype=torch.uint8, device=x.device)
+    check(_lib.load().dllm_quantize_tensor_with_params(_ptr(x) if n else None, n, bits, int(packed), _ptr(pr),
+                                                       _ptr(out) if out.numel() else None, _stream()))
+    return out
+
+
 def dequantize_tensor(codes: torch.Tensor, scale, zero_point=None, *, bits: int = 8, packed: bool = False,
                       n: int | None = None, out_dtype=torch.float32) -> torch.Tensor:
     """quantization.rs:81-85 ``dequantize_tensor(data, scale, zero_point)``.

@@ -81,6 +81,19 @@ int dllm_quantize_tensor_pair(const float *x, size_t n, uint8_t bits_a, uint8_t 
                               float *params_a, uint8_t *out_b, float *params_b, void *workspace,
                               size_t workspace_bytes, dllm_stream_t stream);
 
+/* quantize_tensor split at its one reduction, for a tensor sharded over ranks (the KV
+ * cache sharded by head needs the per-tensor scale of quantization.rs:41-56 over ALL shards).
+ * The extremes fold (:41-46, NaN-ignoring) is order-independent, so each rank folds its shard into
+ * stats[2] = {min, max} (device, seeded {+inf, -inf} by the caller), the ranks combine them with one
+ * all-reduce (max over {-min, max}), and each rank then writes the params (:49-56) and codes
+ * (:59-65) that dllm_quantize_tensor of the whole tensor writes for its elements, bit for bit.
+ * Workspace: dllm_quantize_tensor_workspace(n).  bits outside 1..=8 -> INVALID_PARAMS. */
+int dllm_tensor_extremes(const float *x, size_t n, float *stats, void *workspace, size_t workspace_bytes,
+                         dllm_stream_t stream);
+int dllm_quantize_params_from_extremes(const float *stats, uint8_t bits, float *params, dllm_stream_t stream);
+int dllm_quantize_tensor_with_params(const float *x, size_t n, uint8_t bits, int packed, const float *params,
+                                     uint8_t *out, dllm_stream_t stream);
+
 /* dequantize_tensor(data: &[u8], scale: f32, zero_point: f32) -> Vec<f32> (quantization.rs:81-85)
  * and QuantizedTensor::dequantize (:115-117):  y = ((q as f32) - zp) * scale.
  * params[2] = {scale, zp} in DEVICE memory (as written by dllm_quantize_tensor).

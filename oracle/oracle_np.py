@@ -58,23 +58,34 @@ def fold_min(x: np.ndarray) -> F32:
 
 # ---- a1 / a2: diffuse-llm-rs/src/quantization.rs -------------------------------------------
 
+def params_from_extremes(mx, mn, bits: int):
+    """quantization.rs:49-56 -> (scale f32, zero_point f32) from the folds of :41-46."""
+    q_min, q_max = F32(0.0), F32(float(1 << bits) - 1.0)
+    with np.errstate(all="ignore"):
+        scale = F32((F32(mx) - F32(mn)) / (q_max - q_min))
+        if scale == F32(0.0):
+            scale = F32(1.0)
+        zpf = F32(q_min - F32(F32(mn) / scale))
+        zp = rs_as_u8(rs_round(rs_clamp(np.array([zpf], F32), q_min, q_max)))[0]
+    return F32(scale), F32(zp)
+
+
+def quantize_with_params(data: np.ndarray, bits: int, scale, zp) -> np.ndarray:
+    """quantization.rs:59-65: the code map once (scale, zero_point) are known."""
+    x = np.asarray(data, dtype=F32).ravel()
+    with np.errstate(all="ignore"):
+        v = (x / F32(scale)).astype(F32)
+        v = (v + F32(zp)).astype(F32)
+        return np.clip(rs_as_i32(rs_round(v)), 0, (1 << bits) - 1).astype(np.uint8)
+
+
 def quantize_tensor(data: np.ndarray, bits: int):
     """quantization.rs:38-68 -> (codes u8, scale f32, zero_point f32)."""
     if not 1 <= bits <= 8:
         raise ValueError("Bits must be between 1 and 8")  # :39 assert!
     x = np.asarray(data, dtype=F32).ravel()
-    mx, mn = fold_max(x), fold_min(x)
-    q_min, q_max = F32(0.0), F32(float(1 << bits) - 1.0)
-    with np.errstate(all="ignore"):
-        scale = F32((mx - mn) / (q_max - q_min))
-        if scale == F32(0.0):
-            scale = F32(1.0)
-        zpf = F32(q_min - F32(mn / scale))
-        zp = rs_as_u8(rs_round(rs_clamp(np.array([zpf], F32), q_min, q_max)))[0]
-        v = (x / scale).astype(F32)
-        v = (v + F32(zp)).astype(F32)
-        q = np.clip(rs_as_i32(rs_round(v)), 0, (1 << bits) - 1).astype(np.uint8)
-    return q, F32(scale), F32(zp)
+    scale, zp = params_from_extremes(fold_max(x), fold_min(x), bits)
+    return quantize_with_params(x, bits, scale, zp), scale, zp
 
 
 def dequantize_tensor(q: np.ndarray, scale, zero_point) -> np.ndarray:

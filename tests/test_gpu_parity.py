@@ -563,3 +563,37 @@ def test_linear_decode_tiles_exact_integers(dllm, torch, orc, bits):
         lin.set_kernel_variant(4)
         assert np.array_equal(host(lin(Xd, out_dtype=torch.float32)), ref), (bits, M, "policy")
     lin.close()
+
+
+@pytest.mark.parametrize("S,H,G,bits", [(1024, 8, 4, 4), (333, 5, 2, 8), (8192, 32, 8, 4)])
+def test_head_parallel_kv_cache_bitexact(dllm, torch, orc, S, H, G, bits):
+    """K/V sharded by head over G ranks, emulated in one process with the HIP ops of
+    parallel.HeadParallelKVCache (the all_reduce(MAX) of the per-rank extremes is a torch max here).
+    Each shard's params equal the unsharded per-tensor params bit for bit, its packed codes equal
+    the unsharded codes of its heads, and its attention equals the unsharded call's heads."""
+    par = dllm.parallel
+    rng = np.random.default_rng(S + H + G)
+    K = rng.standard_normal((S, H, 128), dtype=np.float32)
+    V = (rng.standard_normal((S, H, 128), dtype=np.float32) * 2 + 0.5).astype(np.float32)
+    Q = rng.standard_normal((S, H, 128), dtype=np.float32).astype(np.float16)
+    Kd, Vd, Qd = dev(torch, K), dev(torch, V), dev(torch, Q)
+    full = dllm.QuantizedKVCacheEntry.new(Kd, Vd, bits)
+    O_full = dllm.kv_attention(Qd, full.keys, full.values)
+    ranks = []
+    for r in range(G):
+        kv = par.HeadParallelKVCache(H, bits)
+        kv.world, kv.rank = G, r
+        kv.h0, kv.h1 = par.head_range(H, G, r)
+        loc = [t[:, kv.h0:kv.h1].contiguous() for t in (Qd, Kd, Vd)]
+        ranks.append((kv, loc, kv.local_extremes(loc[1], loc[2])))
+    red = torch.stack([x[2] for x in ranks]).amax(dim=0)
+    codes_full = [dllm.unpack(t.data, S * H * 128, bits).reshape(S, H, 128) for t in (full.keys, full.values)]
+    for kv, loc, _ in ranks:
+        kc, kp, vc, vp = kv.quantize_with_extremes(loc[1], loc[2], red)
+        n = S * (kv.h1 - kv.h0) * 128
+        for c, p, ref_t, ref_c in ((kc, kp, full.keys, codes_full[0]), (vc, vp, full.values, codes_full[1])):
+            assert same_bits(host(p), host(ref_t.params))
+            assert torch.equal(dllm.unpack(c, n, bits).reshape(S, -1, 128), ref_c[:, kv.h0:kv.h1])
+        e = kv.entry(loc[1], loc[2], red)
+        O = kv.attention(loc[0], e)
+        assert torch.equal(O, O_full[:, kv.h0:kv.h1]), "per-head attention must not depend on the shard"
