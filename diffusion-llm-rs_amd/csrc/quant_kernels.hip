@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <cstdlib>
 
 namespace dllm {
 namespace {
@@ -181,15 +182,19 @@ __global__ void __launch_bounds__(kBlock) minmax_partial_kernel(const float *__r
 }
 
 // (scale, zp) from the extremes exactly as quantization.rs:49-56.
-__device__ __forceinline__ void write_params(float mx, float mn, int bits, float *params) {
+__device__ __forceinline__ void params_of(float mx, float mn, int bits, float &scale_out, float &zp_out) {
     const float q_min = 0.0f;
     const float q_max = static_cast<float>(1u << bits) - 1.0f;     // :50
     float scale = (mx - mn) / (q_max - q_min);                      // :52
     if (scale == 0.0f) scale = 1.0f;                                // :53
     const float zpf = q_min - mn / scale;                           // :55
     const uint32_t zp = rs_as_u8(roundf(rs_clamp(zpf, q_min, q_max)));  // :56
-    params[0] = scale;
-    params[1] = static_cast<float>(zp);                             // :67
+    scale_out = scale;
+    zp_out = static_cast<float>(zp);                                // :67
+}
+
+__device__ __forceinline__ void write_params(float mx, float mn, int bits, float *params) {
+    params_of(mx, mn, bits, params[0], params[1]);
 }
 
 // Params of width `bits` from caller-held extremes stats[2] = {min, max} (sharded quantize_tensor).
@@ -210,6 +215,140 @@ __global__ void __launch_bounds__(kBlock) quant_params_kernel(const float2 *__re
         write_params(mx, mn, bits, params);
         if (bits_b) write_params(mx, mn, bits_b, params_b);
     }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K2 fast path: the quantize map of quantization.rs:59-65 for packed 1/2/4/8-bit codes, with the
+// params reduction (:41-56) folded into every block's prologue and a cheaper exact division.
+// ---------------------------------------------------------------------------------------------
+// x / s exactly as the IEEE division (what Rust's `x / scale` computes), in three FMA-pipe ops
+// instead of the ~10 of the v_div_scale/v_div_fmas/v_div_fixup sequence.  Markstein's theorem:
+// with r = RN(1/s), q0 = RN(x r) is faithful, the residual e = x - q0 s is exact (one fma), and
+// q1 = RN(q0 + e r) = RN(x / s) -- provided nothing over- or underflows.  The callers only use
+// it for s in [2^-64, 2^64] (checked per tensor; otherwise the plain division runs):
+//  * |x/s| >= 2^-25 implies |x| >= 2^-89, so q0, e (>= ~|x| 2^-24) and q1 are normal and exact as
+//    the theorem needs.  A quotient below 2^-25 cannot move a code: round(q) = 0 when zp = 0, and
+//    q + zp rounds to zp when zp >= 1, for the exact and the corrected quotient alike.
+//  * x = +-inf or a quotient that overflows gives e = -+inf and q1 = NaN: the select keeps q0 =
+//    +-inf, whose code (clamped to q_max) equals the code of the IEEE quotient.  x = NaN -> NaN.
+// The identity is also checked exhaustively over all 2^24 significands of x for 1500 divisors
+// (tests/test_quantize_division.py) and bit-exactly on the device by the a1 parity tests.
+__device__ __forceinline__ bool markstein_ok(float s) { return s >= 0x1p-64f && s <= 0x1p64f; }
+
+template <bool kFast>
+__device__ __forceinline__ float div_scale(float x, float s, float r) {
+    if constexpr (!kFast) {
+        return x / s;
+    } else {
+        const float q0 = x * r;
+        const float e = __builtin_fmaf(-q0, s, x);
+        const float q1 = __builtin_fmaf(e, r, q0);
+        return q1 != q1 ? q0 : q1;
+    }
+}
+
+// (round(t) as i32).clamp(0, hi) with Rust's round-half-away-from-zero: trunc(t), plus one when
+// the (exact) fraction t - trunc(t) is >= 0.5; negatives and NaN give 0, +inf gives hi.
+__device__ __forceinline__ uint32_t code_of(float t, uint32_t hi) {
+    const float tr = __builtin_truncf(t);
+    const float c = fminf(fmaxf(tr, 0.0f), static_cast<float>(hi));
+    const uint32_t u = static_cast<uint32_t>(c) + ((t - tr) >= 0.5f ? 1u : 0u);
+    return u > hi ? hi : u;
+}
+
+// Every block folds the min/max partials (order-independent, so each block gets the same
+// extremes bit for bit) and broadcasts them through LDS.
+__device__ __forceinline__ void fold_partials(const float2 *__restrict__ partials, int np, float *smem, float &mx,
+                                              float &mn) {
+    mx = -INFINITY;
+    mn = INFINITY;
+    for (int i = threadIdx.x; i < np; i += kBlock) { float2 p = partials[i]; mx = fmaxf(mx, p.x); mn = fminf(mn, p.y); }
+    block_minmax(mx, mn, smem);
+    if (threadIdx.x == 0) { smem[0] = mx; smem[1] = mn; }
+    __syncthreads();
+    mx = smem[0];
+    mn = smem[1];
+}
+
+template <int B>
+__device__ __forceinline__ void store_packed(uint8_t *__restrict__ out, size_t o, const uint32_t (&c)[8]) {
+    if constexpr (B == 8) {
+        const uint32_t lo = c[0] | (c[1] << 8) | (c[2] << 16) | (c[3] << 24);
+        const uint32_t hi = c[4] | (c[5] << 8) | (c[6] << 16) | (c[7] << 24);
+        *reinterpret_cast<uint2 *>(out + o * 8) = make_uint2(lo, hi);
+    } else {
+        uint32_t w = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) w |= c[i] << (i * B);
+        if constexpr (B == 4) *reinterpret_cast<uint32_t *>(out + o * 4) = w;
+        else if constexpr (B == 2) *reinterpret_cast<uint16_t *>(out + o * 2) = static_cast<uint16_t>(w);
+        else out[o] = static_cast<uint8_t>(w);
+    }
+}
+
+template <int BA, int BB, bool kFast>
+__device__ __forceinline__ void quantize_fused_body(const float *__restrict__ x, size_t n, uint8_t *__restrict__ out_a,
+                                                    uint8_t *__restrict__ out_b, float sa, float za, float sb,
+                                                    float zb) {
+    const float ra = 1.0f / sa, rb = BB ? 1.0f / sb : 0.0f;
+    constexpr uint32_t ha = (1u << BA) - 1u, hb = BB ? (1u << BB) - 1u : 0u;
+    const size_t nfull = n / 8;
+    const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+    auto one = [&](size_t o, const float4 &p0, const float4 &p1) {
+        const float v[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+        uint32_t ca[8], cb[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            ca[i] = code_of(div_scale<kFast>(v[i], sa, ra) + za, ha);   // :61-64
+            if constexpr (BB != 0) cb[i] = code_of(div_scale<kFast>(v[i], sb, rb) + zb, hb);
+        }
+        store_packed<BA>(out_a, o, ca);
+        if constexpr (BB != 0) store_packed<BB>(out_b, o, cb);
+    };
+    size_t o = blockIdx.x * static_cast<size_t>(kBlock) + threadIdx.x;
+    const float4 *x4 = reinterpret_cast<const float4 *>(x);
+    for (; o + stride < nfull; o += 2 * stride) {       // two octets in flight per thread
+        const float4 a0 = x4[2 * o], a1 = x4[2 * o + 1];
+        const float4 b0 = x4[2 * (o + stride)], b1 = x4[2 * (o + stride) + 1];
+        one(o, a0, a1);
+        one(o + stride, b0, b1);
+    }
+    if (o < nfull) one(o, x4[2 * o], x4[2 * o + 1]);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && n % 8) {  // partial tail octet
+        const size_t ot = nfull;
+        const int cnt = static_cast<int>(n - ot * 8);
+        uint32_t ca[8] = {0, 0, 0, 0, 0, 0, 0, 0}, cb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int i = 0; i < cnt; ++i) {
+            const float v = x[ot * 8 + i];
+            ca[i] = code_of(div_scale<kFast>(v, sa, ra) + za, ha);
+            if constexpr (BB != 0) cb[i] = code_of(div_scale<kFast>(v, sb, rb) + zb, hb);
+        }
+        store_codes(out_a, ot, cnt, ca, BA, true, false);
+        if constexpr (BB != 0) store_codes(out_b, ot, cnt, cb, BB, true, false);
+    }
+}
+
+// quantize_tensor (and the pair of widths of KVCacheEntry::update) after minmax_partial_kernel:
+// x 16-B aligned, packed codes (out 8-B aligned); block 0 publishes the params.
+template <int BA, int BB>
+__global__ void __launch_bounds__(kBlock) quantize_fused_kernel(const float *__restrict__ x, size_t n,
+                                                                const float2 *__restrict__ partials, int np,
+                                                                uint8_t *__restrict__ out_a, float *__restrict__ params_a,
+                                                                uint8_t *__restrict__ out_b,
+                                                                float *__restrict__ params_b) {
+    __shared__ float smem[2 * kBlock / 64];
+    float mx, mn, sa, za, sb = 1.0f, zb = 0.0f;
+    fold_partials(partials, np, smem, mx, mn);
+    params_of(mx, mn, BA, sa, za);
+    if constexpr (BB != 0) params_of(mx, mn, BB, sb, zb);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        params_a[0] = sa; params_a[1] = za;
+        if constexpr (BB != 0) { params_b[0] = sb; params_b[1] = zb; }
+    }
+    if (markstein_ok(sa) && (BB == 0 || markstein_ok(sb)))
+        quantize_fused_body<BA, BB, true>(x, n, out_a, out_b, sa, za, sb, zb);
+    else
+        quantize_fused_body<BA, BB, false>(x, n, out_a, out_b, sa, za, sb, zb);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -551,6 +690,44 @@ inline int launch_minmax(const float *x, size_t n, float2 *partials, unsigned nb
 
 inline unsigned minmax_blocks(size_t n) { return grid_for((n + 15) / 16, kBlock, kMinmaxBlocks); }
 
+// DLLM_QUANT_GENERIC=1 selects the generic two-kernel path (A/B measurement and parity tests).
+inline bool fused_disabled() {
+    const char *e = std::getenv("DLLM_QUANT_GENERIC");
+    return e && e[0] == '1';
+}
+
+inline bool fused_width(int b) { return b == 1 || b == 2 || b == 4 || b == 8; }
+
+// Grid of quantize_fused_kernel: two full octets per thread per trip, at most 8 blocks per CU
+// (all resident, so the prologue's 8 KiB partials read overlaps other blocks' streaming).
+inline unsigned fused_grid(size_t n) { return grid_for((n / 8 + 1) / 2, kBlock, kCUs * 8); }
+
+template <int BA>
+int launch_fused_b(const float *x, size_t n, const float2 *partials, int np, uint8_t *out_a, float *params_a, int bb,
+                   uint8_t *out_b, float *params_b, hipStream_t st) {
+    const unsigned g = fused_grid(n);
+    switch (bb) {
+    case 0: quantize_fused_kernel<BA, 0><<<g, kBlock, 0, st>>>(x, n, partials, np, out_a, params_a, out_b, params_b); break;
+    case 1: quantize_fused_kernel<BA, 1><<<g, kBlock, 0, st>>>(x, n, partials, np, out_a, params_a, out_b, params_b); break;
+    case 2: quantize_fused_kernel<BA, 2><<<g, kBlock, 0, st>>>(x, n, partials, np, out_a, params_a, out_b, params_b); break;
+    case 4: quantize_fused_kernel<BA, 4><<<g, kBlock, 0, st>>>(x, n, partials, np, out_a, params_a, out_b, params_b); break;
+    default: quantize_fused_kernel<BA, 8><<<g, kBlock, 0, st>>>(x, n, partials, np, out_a, params_a, out_b, params_b); break;
+    }
+    DLLM_LAUNCH_CHECK();
+    return DLLM_OK;
+}
+
+// bits_b = 0: one width.  Preconditions: fused_width(bits_a) (and bits_b), x 16-B and outs 8-B aligned.
+inline int launch_fused(const float *x, size_t n, const float2 *partials, int np, int bits_a, uint8_t *out_a,
+                        float *params_a, int bits_b, uint8_t *out_b, float *params_b, hipStream_t st) {
+    switch (bits_a) {
+    case 1: return launch_fused_b<1>(x, n, partials, np, out_a, params_a, bits_b, out_b, params_b, st);
+    case 2: return launch_fused_b<2>(x, n, partials, np, out_a, params_a, bits_b, out_b, params_b, st);
+    case 4: return launch_fused_b<4>(x, n, partials, np, out_a, params_a, bits_b, out_b, params_b, st);
+    default: return launch_fused_b<8>(x, n, partials, np, out_a, params_a, bits_b, out_b, params_b, st);
+    }
+}
+
 }  // namespace
 }  // namespace dllm
 
@@ -575,6 +752,9 @@ int dllm_quantize_tensor(const float *x, size_t n, uint8_t bits, int packed, uin
     if (n) {
         int rc = launch_minmax(x, n, partials, nblk, st);
         if (rc) return rc;
+        if (packed && fused_width(bits) && aligned(x, 16) && aligned(out, 8) && !fused_disabled())
+            return launch_fused(x, n, partials, static_cast<int>(nblk), bits, out, params_out, 0, nullptr, nullptr,
+                                st);
     }
     quant_params_kernel<<<1, kBlock, 0, st>>>(partials, n ? static_cast<int>(nblk) : 0, bits, params_out);
     DLLM_LAUNCH_CHECK();
@@ -600,6 +780,10 @@ int dllm_quantize_tensor_pair(const float *x, size_t n, uint8_t bits_a, uint8_t 
     if (n) {
         int rc = launch_minmax(x, n, partials, nblk, st);
         if (rc) return rc;
+        if (packed && fused_width(bits_a) && fused_width(bits_b) && aligned(x, 16) && aligned(out_a, 8) &&
+            aligned(out_b, 8) && !fused_disabled())
+            return launch_fused(x, n, partials, static_cast<int>(nblk), bits_a, out_a, params_a, bits_b, out_b,
+                                params_b, st);
     }
     quant_params_kernel<<<1, kBlock, 0, st>>>(partials, n ? static_cast<int>(nblk) : 0, bits_a, params_a, bits_b,
                                               params_b);

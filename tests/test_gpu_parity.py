@@ -102,6 +102,49 @@ def test_quantize_tensor_pair_matches_two_calls(dllm, torch, orc, n):
     assert same_bits(host(p4), np.array([s, z], np.float32))
 
 
+def _scaled_tensors(rng):
+    """Inputs whose per-tensor scale falls on either side of the fused kernel's exact-division
+    guard [2^-64, 2^64] (inside it the corrected reciprocal product runs, outside the IEEE division),
+    plus quotients on rounding ties, inf/NaN elements and an all-positive tensor."""
+    base = rng.standard_normal(4099).astype(np.float32)
+    out = {}
+    for e in (-90, -66, -64, -63, -10, 0, 10, 62, 63, 64, 66, 90):
+        out[f"range2^{e}"] = (base * np.float32(2.0 ** e)).astype(np.float32)
+    ties = np.arange(31, dtype=np.float32) * np.float32(2.0 ** -4)   # 4-bit: s = 1/8, x/s = k/2
+    out["ties"] = np.tile(ties, 37)
+    special = base.copy()
+    special[[5, 77, 1000]] = [np.inf, -np.inf, np.nan]
+    out["inf_nan"] = special
+    out["positive"] = (np.abs(base) + np.float32(1000.0)).astype(np.float32)
+    return out
+
+
+def test_quantize_fused_path_scale_guard(dllm, torch, orc, monkeypatch):
+    """The fused quantize kernel (params folded into the prologue, Markstein division) is the
+    default for packed 1/2/4/8-bit codes from a 16-B aligned x; it must give the oracle's codes and
+    params bit for bit on both sides of its division guard, alone and as a pair of widths, and the
+    same bytes as the generic two-kernel path (DLLM_QUANT_GENERIC=1)."""
+    rng = np.random.default_rng(2024)
+    for name, x in _scaled_tensors(rng).items():
+        xd = dev(torch, x)
+        assert xd.data_ptr() % 16 == 0
+        for bits in (1, 2, 4, 8):
+            q, params = dllm.quantize_tensor(xd, bits, packed=True)
+            rq, rs, rz = orc.quantize_tensor(x, bits)
+            assert np.array_equal(host(q), orc.pack_bits(rq, bits)), (name, bits)
+            assert same_bits(host(params), np.array([rs, rz], np.float32)), (name, bits)
+        for ba, bb in ((4, 2), (8, 4), (2, 1)):
+            (ca, pa), (cb, pb) = dllm.quantize_tensor_pair(xd, ba, bb, packed=True)
+            for c, pr, b in ((ca, pa, ba), (cb, pb, bb)):
+                rq, rs, rz = orc.quantize_tensor(x, b)
+                assert np.array_equal(host(c), orc.pack_bits(rq, b)), (name, ba, bb, b)
+                assert same_bits(host(pr), np.array([rs, rz], np.float32)), (name, ba, bb, b)
+            monkeypatch.setenv("DLLM_QUANT_GENERIC", "1")
+            (ga, _), (gb, _) = dllm.quantize_tensor_pair(xd, ba, bb, packed=True)
+            monkeypatch.delenv("DLLM_QUANT_GENERIC")
+            assert torch.equal(ga, ca) and torch.equal(gb, cb), (name, ba, bb)
+
+
 def test_dequantize_scalar_signature(dllm, torch, orc):
     rng = np.random.default_rng(1)
     q = rng.integers(0, 16, 777).astype(np.uint8)
