@@ -77,11 +77,23 @@ def cpu_baseline(K, N, bits, group, M, budget_s):
     orc.linear_forward(X, What, b, nthreads=1)
     t_rows = time.perf_counter() - t0
     t_step = t_deq + t_rows / rows * M
+    # the same restatement on the host cores of this job's share (the GPU box
+    # gives one GPU 16 CPUs; os.cpu_count() there shows the whole machine), rows split by thread.
+    threads = max(1, min(16, os.cpu_count() or 1))
+    rows_mt = int(max(threads, min(M, rows * threads)))
+    Xm = rng.standard_normal((rows_mt, K)).astype(np.float32)
+    t0 = time.perf_counter()
+    orc.linear_forward(Xm, What, b, nthreads=threads)
+    t_mt = time.perf_counter() - t0
+    t_step_mt = t_deq + t_mt / rows_mt * M
+    all_cores = {"value": M / t_step_mt, "unit": "tok/s", "cores": threads,
+                 "sample": f"same restatement, {threads} threads: {rows_mt} of {M} rows ({t_mt:.2f}s), "
+                           f"step extrapolated to {M} rows = {t_step_mt:.2f}s"}
     return {"value": M / t_step, "unit": "tok/s", "cores": 1, "kind": "port",
             "sample": f"C restatement (oracle/dllm_oracle.c), 1 thread: a2 dequant of the {K}x{N} int{bits} "
                       f"g{group} weight ({t_deq:.3f}s) + f32 sgemm+bias on {rows} of {M} rows "
                       f"({t_rows:.2f}s), step time extrapolated to {M} rows = {t_step:.2f}s",
-            "host_cpu": _cpu_model(), "nproc": os.cpu_count()}
+            "host_cpu": _cpu_model(), "nproc": os.cpu_count(), "all_cores": all_cores}
 
 
 def _cpu_model():
