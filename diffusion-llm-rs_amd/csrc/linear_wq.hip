@@ -91,6 +91,78 @@ __global__ void __launch_bounds__(256) quantize_weights_kernel(const float *__re
     }
 }
 
+// Same results as quantize_weights_kernel without its per-code atomics (N % 4 == 0, group <= 128):
+// lane = 16 r + c of a wave owns column quad c (4 columns, one float4 per row) and rows
+// [32 r, 32 r + 32) of the group, held in registers between the two passes; the group's extremes
+// (order-independent NaN-ignoring folds, so identical to the serial fold) are combined across the
+// 4 row quarters by two xor-shuffles, and each lane writes whole canonical bytes (4 codes of a row).
+__global__ void __launch_bounds__(256) quantize_weights4_kernel(const float *__restrict__ W, size_t K, size_t N,
+                                                                int bits, int group, uint32_t *__restrict__ canon,
+                                                                float *__restrict__ scales,
+                                                                uint8_t *__restrict__ zps) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const size_t n = (static_cast<size_t>(blockIdx.x) * 4 + wave) * 64 + 4 * (lane & 15);
+    const size_t g = blockIdx.y;
+    const size_t k0 = g * group;
+    const int len = static_cast<int>(std::min<size_t>(group, K - k0));
+    const int r0 = 32 * (lane >> 4);
+    const bool col_ok = n < N;
+    float4 v[32];
+    float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY}, mn[4] = {INFINITY, INFINITY, INFINITY, INFINITY};
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+        const bool ok = col_ok && r0 + i < len;
+        v[i] = ok ? *reinterpret_cast<const float4 *>(W + (k0 + r0 + i) * N + n) : make_float4(NAN, NAN, NAN, NAN);
+    }
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {                              // quantization.rs:41-46
+        mx[0] = fmaxf(mx[0], v[i].x); mn[0] = fminf(mn[0], v[i].x);
+        mx[1] = fmaxf(mx[1], v[i].y); mn[1] = fminf(mn[1], v[i].y);
+        mx[2] = fmaxf(mx[2], v[i].z); mn[2] = fminf(mn[2], v[i].z);
+        mx[3] = fmaxf(mx[3], v[i].w); mn[3] = fminf(mn[3], v[i].w);
+    }
+    float scale[4], zpf32[4];
+    const float q_max = static_cast<float>(1u << bits) - 1.0f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        mx[j] = fmaxf(mx[j], __shfl_xor(mx[j], 16, 64));
+        mx[j] = fmaxf(mx[j], __shfl_xor(mx[j], 32, 64));
+        mn[j] = fminf(mn[j], __shfl_xor(mn[j], 16, 64));
+        mn[j] = fminf(mn[j], __shfl_xor(mn[j], 32, 64));
+        float sc = (mx[j] - mn[j]) / (q_max - 0.0f);            // :52
+        if (sc == 0.0f) sc = 1.0f;                              // :53
+        const float zpf = 0.0f - mn[j] / sc;                    // :55
+        const uint32_t zp = rs_as_u8(roundf(rs_clamp(zpf, 0.0f, q_max)));   // :56
+        scale[j] = sc;
+        zpf32[j] = static_cast<float>(zp);
+    }
+    if (!col_ok) return;
+    if (r0 == 0) {
+        *reinterpret_cast<float4 *>(scales + g * N + n) = make_float4(scale[0], scale[1], scale[2], scale[3]);
+        const uint32_t zq = static_cast<uint32_t>(zpf32[0]) | (static_cast<uint32_t>(zpf32[1]) << 8) |
+                            (static_cast<uint32_t>(zpf32[2]) << 16) | (static_cast<uint32_t>(zpf32[3]) << 24);
+        *reinterpret_cast<uint32_t *>(zps + g * N + n) = zq;
+    }
+    const int hi = (1 << bits) - 1;
+    uint8_t *cb = reinterpret_cast<uint8_t *>(canon);
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {                              // :59-65
+        if (r0 + i >= len) continue;
+        const float e[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+        uint32_t w = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float t = e[j] / scale[j];
+            t = t + zpf32[j];
+            w |= rs_round_i32_clamp(t, hi) << (j * bits);
+        }
+        const size_t byte = ((k0 + r0 + i) * N + n) * bits / 8;
+        if (bits == 2) cb[byte] = static_cast<uint8_t>(w);
+        else if (bits == 4) *reinterpret_cast<uint16_t *>(cb + byte) = static_cast<uint16_t>(w);
+        else *reinterpret_cast<uint32_t *>(cb + byte) = w;
+    }
+}
+
 __device__ __forceinline__ uint32_t canon_code(const uint32_t *__restrict__ canon, size_t k, size_t n, size_t N,
                                                int bits) {
     const size_t bit = (k * N + n) * bits;
@@ -1632,8 +1704,16 @@ int dllm_linear_create(const float *W, const float *bias, size_t K, size_t N, ui
     hipStream_t st = as_stream(stream);
     hipError_t e = hipMemsetAsync(h->canon, 0, canon_words(K, N, bits) * 4, st);
     if (e != hipSuccess) { free_linear(h); return fail(DLLM_ERR_HIP, hipGetErrorString(e)); }
-    dim3 g(static_cast<unsigned>((N + 255) / 256), static_cast<unsigned>(h->G));
-    quantize_weights_kernel<<<g, 256, 0, st>>>(W, K, N, bits, static_cast<int>(group), h->canon, h->scales, h->zps);
+    if (N % 4 == 0 && group <= 128 && (bits == 2 || bits == 4 || bits == 8) &&
+        (reinterpret_cast<uintptr_t>(W) & 15) == 0) {
+        dim3 g(static_cast<unsigned>((N + 255) / 256), static_cast<unsigned>(h->G));
+        quantize_weights4_kernel<<<g, 256, 0, st>>>(W, K, N, bits, static_cast<int>(group), h->canon, h->scales,
+                                                     h->zps);
+    } else {
+        dim3 g(static_cast<unsigned>((N + 255) / 256), static_cast<unsigned>(h->G));
+        quantize_weights_kernel<<<g, 256, 0, st>>>(W, K, N, bits, static_cast<int>(group), h->canon, h->scales,
+                                                    h->zps);
+    }
     if (hipGetLastError() != hipSuccess) { free_linear(h); return fail(DLLM_ERR_HIP, "quantize_weights launch"); }
     if ((rc = finish_linear(h, bias, st))) { free_linear(h); return rc; }
     *out = h;

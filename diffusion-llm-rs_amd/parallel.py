@@ -89,11 +89,26 @@ class RowParallelLinear:
         self.bias = bias
         self.local = local_factory(W[self.k0:self.k1].contiguous(), None, bits, group)
 
-    def forward(self, x: torch.Tensor, out_dtype=torch.float16, x_is_shard: bool = False) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, out_dtype=torch.float16, x_is_shard: bool = False,
+                chunks: int = 1) -> torch.Tensor:
+        """``chunks`` > 1 splits the tokens: the all-reduce of chunk i (asynchronous, on the
+        collective's own stream) runs while the GEMM of chunk i+1 computes (the
+        hidden-dim-sharded loop is communication-bound, so the exchange must hide under compute).
+        Rows are independent, so every chunking gives the same per-row partial sums."""
         xs = x if x_is_shard else x[:, self.k0:self.k1].contiguous()
-        y = self.local(xs, out_dtype=torch.float32)   # partial sums stay f32 until reduced
-        if self.world > 1:
-            dist.all_reduce(y, op=dist.ReduceOp.SUM, group=self.pg)
+        if self.world == 1 or chunks <= 1 or xs.shape[0] < 2:
+            y = self.local(xs, out_dtype=torch.float32)   # partial sums stay f32 until reduced
+            if self.world > 1:
+                dist.all_reduce(y, op=dist.ReduceOp.SUM, group=self.pg)
+        else:
+            parts, works = [], []
+            for xc in torch.tensor_split(xs, min(chunks, xs.shape[0]), dim=0):
+                yc = self.local(xc.contiguous(), out_dtype=torch.float32)
+                works.append(dist.all_reduce(yc, op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
+                parts.append(yc)
+            for w in works:
+                w.wait()
+            y = torch.cat(parts, dim=0)
         if self.bias is not None:
             y = y + self.bias.to(y.device, torch.float32)[None, :]
         return y.to(out_dtype)
@@ -117,9 +132,9 @@ class TensorParallelPair:
         self.b = RowParallelLinear(WB, bB, bits, group, pg, local_factory=local_factory)
         assert (self.b.k0, self.b.k1) == (self.a.n0, self.a.n1)
 
-    def forward(self, x: torch.Tensor, out_dtype=torch.float16) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, out_dtype=torch.float16, chunks: int = 1) -> torch.Tensor:
         h = self.a(x, out_dtype=torch.float16)
-        return self.b(h, out_dtype=out_dtype, x_is_shard=True)
+        return self.b(h, out_dtype=out_dtype, x_is_shard=True, chunks=chunks)
 
     __call__ = forward
 

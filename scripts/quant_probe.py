@@ -15,5 +15,8 @@ k = torch.randn(8192 * 4096, device="cuda")
 for _ in range(n_iter):
     dllm.quantize_tensor(x, 4, packed=True)
     dllm.quantize_tensor_pair(k, 4, 2, packed=True)
+w = 0.02 * torch.randn(4096, 4096, device="cuda")
+for _ in range(5):
+    dllm.QuantLinear.from_weight(w, None, 4, 128)     # a5 weight quantization (quantize_weights4_kernel)
 torch.cuda.synchronize()
 print("done")

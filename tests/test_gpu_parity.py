@@ -276,7 +276,7 @@ def _linear_case(dllm, torch, orc, M, K, N, bits, ydt, seed=0, bias=True):
 
 @pytest.mark.parametrize("M,K,N", [(16, 256, 96), (64, 512, 256), (256, 1024, 512), (300, 640, 200),
                                    (1, 128, 128), (513, 256, 384), (40, 576, 200), (17, 4096, 1024),
-                                   (64, 4096, 4096), (65, 512, 128)])
+                                   (64, 4096, 4096), (65, 512, 128), (8, 256, 130)])
 def test_linear_int4_shapes(dllm, torch, orc, M, K, N):
     for ydt in (torch.float32, torch.float16):
         Y, Yr, _, _ = _linear_case(dllm, torch, orc, M, K, N, 4, ydt)

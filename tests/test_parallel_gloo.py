@@ -68,6 +68,8 @@ def _worker(rank, world, port, outdir):
     res["row_scales"], res["row_range"] = row.local.scales, np.array([row.k0, row.k1])
     pair = par.TensorParallelPair(WA, bA, WB, bB, 4, 128, local_factory=OracleLinear)
     res["pair_y"] = pair(X, out_dtype=torch.float32).numpy()
+    res["pair_y_chunked"] = pair(X, out_dtype=torch.float32, chunks=3).numpy()
+    res["row_y_chunked"] = row(X, out_dtype=torch.float32, chunks=5).numpy()
     tok = par.TokenParallelLinear(WA, bA, 4, 128, local_factory=OracleLinear)
     m0, m1 = tok.token_range(M)
     res["tok_y"], res["tok_range"] = tok(X[m0:m1], out_dtype=torch.float32).numpy(), np.array([m0, m1])
@@ -127,3 +129,11 @@ def test_parallel_outputs_match_unsharded(gloo_results, orc):
     for i, r in enumerate(gloo_results):
         m0, m1 = r["tok_range"]
         np.testing.assert_allclose(r["tok_y"], Y[m0:m1], rtol=0, atol=1e-6)
+
+
+def test_chunked_allreduce_overlap_is_identical(gloo_results):
+    """Row-parallel all-reduce issued per token chunk (async, overlapping the next chunk's GEMM)
+    gives the unchunked result bit for bit: rows are independent and a 2-rank sum is order-free."""
+    for r in gloo_results:
+        assert np.array_equal(r["row_y_chunked"], r["row_y"])
+        assert np.array_equal(r["pair_y_chunked"], r["pair_y"])
