@@ -1586,6 +1586,8 @@ int launch_auto(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t
         }
         return launch_ring<BITS, YT, 8, 8, 1, EPI>(h, X, M, Y, st, 1, epi);
     }
+    if (h->variant == 13 && np % 256 == 0 && 2 * mb256 * (np / 256) >= kCUs && (h->K / kBK) % 2 == 0)
+        return launch_ring<BITS, YT, 8, 8, 1, EPI>(h, X, M, Y, st, 2, epi);   // 256 x 256, K split 2 (A/B)
     const bool kg2 = h->variant != 5;   // variant 5: the same tiles with one k-group (A/B)
     if (mb256 * (np / 128) >= kCUs)
         return kg2 ? launch_ring<BITS, YT, 4, 8, 2, EPI>(h, X, M, Y, st, 1, epi)
@@ -1878,8 +1880,8 @@ int dllm_linear_set_kernel_variant(dllm_linear_t h, int variant) {
         h->pplab = (variant - 100) % 32;
         return DLLM_OK;
     }
-    if (variant < 0 || variant > 12)
-        return fail(DLLM_ERR_INVALID_PARAMS, "variant must be 0..12 (16..23, 32..95, 100..195, 200..263: ablations)");
+    if (variant < 0 || variant > 13)
+        return fail(DLLM_ERR_INVALID_PARAMS, "variant must be 0..13 (16..23, 32..95, 100..195, 200..263: ablations)");
     h->variant = variant;
     h->dlab = h->rlab = h->pplab = h->dcfg = 0;
     return DLLM_OK;

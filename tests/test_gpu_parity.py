@@ -405,6 +405,23 @@ def test_linear_big_tile_exact_integers(dllm, torch, orc, variant, bits):
     lin.close()
 
 
+def test_linear_split_big_tile_exact_integers(dllm, torch, orc):
+    """Variant 13 (A/B only: 256x256 tiles with a 2-way K split + slab reduce, profiles/r01_splitk_ab)
+    at M = 2048, on exact-integer data with bias: bit-equal to the f64 product."""
+    K, N, M = 512, 4096, 2048
+    rng = np.random.default_rng(77)
+    W = rng.integers(0, 16, (K, N)).astype(np.float32)
+    for g0 in range(0, K, 128):     # every group spans [0, 15]: scale 1, zp 0, exact dequant
+        W[g0, :], W[g0 + 1, :] = 0.0, 15.0
+    X = rng.integers(-2, 3, (M, K)).astype(np.float32)
+    b = rng.integers(-4, 5, N).astype(np.float32)
+    lin = dllm.QuantLinear.from_weight(dev(torch, W), dev(torch, b), 4, 128)
+    lin.set_kernel_variant(13)
+    Y = host(lin(dev(torch, X).half(), out_dtype=torch.float32))
+    assert np.array_equal(Y, (X.astype(np.float64) @ W.astype(np.float64) + b).astype(np.float32))
+    lin.close()
+
+
 def test_mixed_precision_stack(dllm, torch, orc):
     """Config 3 shape family: layers cycle bits [2, 4]; each layer within tolerance of the f32
     restatement applied to the same f16 input."""
