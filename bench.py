@@ -42,6 +42,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--sweep", action="store_true", help="also print an M-sweep to stderr")
+    p.add_argument("--no-denoise", action="store_true",
+                   help="skip the config-C5 denoise-loop side measurement (reported as 'denoise_loop')")
     p.add_argument("--prewarm-ms", type=float, default=300.0,
                    help="untimed launches of the same step before the W warmup steps, so the clocks "
                         "have ramped before timing (outside the timed region)")
@@ -117,6 +119,39 @@ def load_pmc_traffic():
         return float(d["hbm_bytes_per_launch"])
     except Exception:
         return None
+
+
+def denoise_loop(d, torch, dev, steps=50):
+    """Config C5 on this rank's GPU (SURVEY.md 8d): DiffuseLLM::sample (diffuse-llm-rs/src/lib.rs:853-955)
+    over 12 int4 g128 layers of d 4096 at seq 2048, 50 steps, KV-cache update + noise on the side stream,
+    p_sample fused into the last layer.  Weights 0.5/sqrt(d) N(0,1) keep the 50-step recursion finite
+    (the reference's 0.02 N(0,1) overflows f32 in a 12-layer stack; the kernels do the same work).
+    A side figure next to `value`, timed with HIP events on the loop's stream."""
+    dm, M, L = 4096, 2048, 12
+    g = torch.Generator(device=dev).manual_seed(99)
+    layers = [d.QuantLinear.from_weight((0.5 / 64.0) * torch.randn(dm, dm, device=dev, generator=g), None, 4, 128)
+              for _ in range(L)]
+    cfg = d.DiffusionConfig(num_timesteps=steps, hidden_size=dm, num_layers=L)
+    kv = d.KVCacheEntry.new(torch.randn(1, M, dm, device=dev, generator=g),
+                            torch.randn(1, M, dm, device=dev, generator=g), cfg.prefill_bits, cfg.decode_bits)
+    loop = d.DenoiseLoop(layers, cfg, cumprod=d.Cumprod.INCLUSIVE, seed=1, kv_cache=kv, overlap=True)
+    x = torch.randn(M, dm, device=dev, generator=g)
+    loop.sample(x, 3)
+    torch.cuda.synchronize()
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    out = loop.sample(x, steps)
+    e1.record(st)
+    torch.cuda.synchronize()
+    s = e0.elapsed_time(e1) * 1e-3
+    res = {"workload": f"C5: {L} x int4-g128 d{dm} layers, seq {M}, {steps} steps, KV update + fused p_sample, 1 GPU",
+           "ms_per_step": round(s / steps * 1e3, 4), "tok_per_s_per_step": round(M / (s / steps), 1),
+           "gemm_tflops": round(steps * L * 2 * M * dm * dm / s / 1e12, 1),
+           "finite": bool(torch.isfinite(out).all())}
+    for lyr in layers:
+        lyr.close()
+    return res
 
 
 def main():
@@ -195,6 +230,8 @@ def main():
                      "traffic": load_pmc_traffic(), "algorithmic_bytes": abytes,
                      "kernel_ms": round(kernel_ms, 5)},
     }
+    if not args.no_denoise:
+        out["denoise_loop"] = denoise_loop(d, torch, dev)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(K, N, args.bits, args.group, M, args.cpu_seconds)
     if rank == 0:

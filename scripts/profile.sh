@@ -16,7 +16,7 @@ IFS=';' read -ra SETARR <<< "$SETS"
 for C in "${SETARR[@]}"; do
   tag=$(echo $C | cut -d' ' -f1)
   [ -n "$tag" ] || continue
-  timeout -k 10 300 rocprofv3 --pmc $C --kernel-include-regex "${KREGEX:-wq_gemm}" -d "$OUT/pmc_$tag" -o pmc --output-format csv -- python3 bench.py ${PMC_BENCH_ARGS:---steps 5 --warmup 2 --no-cpu --prewarm-ms 0} > "$OUT/pmc_$tag.log" 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $C --kernel-include-regex "${KREGEX:-wq_gemm}" -d "$OUT/pmc_$tag" -o pmc --output-format csv -- python3 bench.py ${PMC_BENCH_ARGS:---steps 5 --warmup 2 --no-cpu --no-denoise --prewarm-ms 0} > "$OUT/pmc_$tag.log" 2>&1
   rc=$?; echo "pmc $tag rc=$rc"; tail -2 "$OUT/pmc_$tag.log"
   case $rc in 124|134|137|139) echo "hard failure; stopping"; exit $rc;; esac
 done
