@@ -283,6 +283,36 @@ def test_linear_int4_shapes(dllm, torch, orc, M, K, N):
         assert rel_err(Y, Yr) <= REL_TOL, (M, K, N, ydt, rel_err(Y, Yr))
 
 
+@pytest.mark.parametrize("bits,group,K,N,misalign", [
+    (4, 128, 640, 256, False), (2, 128, 576, 200, False), (8, 64, 320, 132, False),   # register kernel
+    (4, 128, 448, 96, False),                                                         # ragged last group
+    (4, 192, 640, 256, False), (4, 128, 512, 130, False), (2, 128, 256, 256, True)])  # atomicOr fallback
+def test_weight_quantization_bit_exact(dllm, torch, orc, bits, group, K, N, misalign):
+    """a5 weight quantization (a1 per column-group, quantization.rs:38-68) on both device kernels
+    (quantize_weights4_kernel: N % 4 == 0, group <= 128, 16-B aligned W; otherwise the atomicOr
+    kernel) vs the oracle, bit for bit, with NaN, +-inf, +-0 and constant column-groups."""
+    rng = np.random.default_rng(bits * 1000 + group + K + N)
+    W = (0.02 * rng.standard_normal((K, N))).astype(np.float32)
+    W[3, 5], W[7, 1], W[K - 1, N - 1] = np.nan, np.inf, -np.inf
+    W[:group, 2] = 0.25                        # constant group: scale 1.0 (quantization.rs:53)
+    W[:, 3] = -0.0
+    W[group - 1, 4] = np.nan                   # NaN on the last row of a group
+    codes, scales, zps = orc.quantize_weights(W, bits, group)
+    if misalign:
+        buf = torch.empty(K * N + 1, dtype=torch.float32, device="cuda")
+        buf[1:].copy_(torch.from_numpy(W.ravel()).cuda())
+        Wd = buf[1:].view(K, N)
+        assert Wd.data_ptr() % 16 != 0
+    else:
+        Wd = dev(torch, W)
+    lin = dllm.QuantLinear.from_weight(Wd, None, bits, group)
+    pc, ps, pz = lin.export()
+    assert np.array_equal(host(pc), orc.pack_bits(codes.ravel(), bits)), "weight codes differ"
+    assert same_bits(host(ps), scales), "weight scales differ"
+    assert np.array_equal(host(pz), zps), "weight zero points differ"
+    lin.close()
+
+
 @pytest.mark.parametrize("bits", [2, 8])
 def test_linear_other_widths(dllm, torch, orc, bits):
     Y, Yr, _, _ = _linear_case(dllm, torch, orc, 128, 512, 256, bits, torch.float32, seed=bits)
