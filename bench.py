@@ -42,6 +42,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--sweep", action="store_true", help="also print an M-sweep to stderr")
+    p.add_argument("--tp-steps", type=int, default=10,
+                   help="N > 1: steps of the hidden-dim-sharded C5 loop reported as 'denoise_loop_tp' (0 skips)")
     p.add_argument("--no-denoise", action="store_true",
                    help="skip the config-C5 denoise-loop side measurement (reported as 'denoise_loop')")
     p.add_argument("--prewarm-ms", type=float, default=300.0,
@@ -154,6 +156,44 @@ def denoise_loop(d, torch, dev, steps=50):
     return res
 
 
+def denoise_loop_tp(d, torch, dist, dev, world, steps):
+    """Config C5 hidden-dim sharded over the job's ranks: 12 int4 layers as 6
+    Megatron pairs (parallel.TensorParallelPair: column shard, row shard, one all-reduce(sum) of the
+    f32 partial [2048, 4096] per pair over RCCL), p_sample after the last pair, no KV cache.
+    Every rank builds the same full weights (seeded) and keeps its shard.  Timed with a barrier and
+    synchronize on both sides, max over ranks."""
+    par = d.parallel
+    dm, M, L = 4096, 2048, 12
+    g = torch.Generator(device=dev).manual_seed(99)
+    pairs = []
+    for _ in range(L // 2):
+        WA = (0.5 / 64.0) * torch.randn(dm, dm, device=dev, generator=g)
+        WB = (0.5 / 64.0) * torch.randn(dm, dm, device=dev, generator=g)
+        pairs.append(par.TensorParallelPair(WA, None, WB, None, 4, 128))
+        del WA, WB
+    cfg = d.DiffusionConfig(num_timesteps=steps, hidden_size=dm, num_layers=L)
+    loop = d.DenoiseLoop(pairs, cfg, cumprod=d.Cumprod.INCLUSIVE, seed=1, kv_cache=None, overlap=False)
+    x = torch.randn(M, dm, device=dev, generator=g)
+    loop.sample(x, 2)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    out = loop.sample(x, steps)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    s = float(t.item())
+    res = {"workload": f"C5 hidden-dim sharded: {L // 2} TensorParallelPair of int4-g128 d{dm}, seq {M}, "
+                       f"{steps} steps, one all-reduce (f32 [{M}, {dm}]) per pair, p_sample, no KV cache",
+           "n_ranks": world, "ms_per_step": round(s / steps * 1e3, 4),
+           "tok_per_s_per_step": round(M / (s / steps), 1), "finite": bool(torch.isfinite(out).all())}
+    for p in pairs:
+        p.a.local.close()
+        p.b.local.close()
+    return res
+
+
 def main():
     args = parse()
     import torch
@@ -162,9 +202,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # DLLM_BENCH_BACKEND=gloo + device = local % device_count: a rehearsal of the N > 1 path with
+    # several ranks on one GPU (the driver's multi-GPU runs use RCCL, one GPU per rank).
+    backend = os.environ.get("DLLM_BENCH_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
 
     import __graft_entry__ as g
@@ -232,6 +279,8 @@ def main():
     }
     if not args.no_denoise:
         out["denoise_loop"] = denoise_loop(d, torch, dev)
+        if world > 1 and args.tp_steps > 0:
+            out["denoise_loop_tp"] = denoise_loop_tp(d, torch, dist, dev, world, args.tp_steps)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(K, N, args.bits, args.group, M, args.cpu_seconds)
     if rank == 0:
