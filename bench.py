@@ -174,20 +174,26 @@ def denoise_loop_tp(d, torch, dist, dev, world, steps):
     cfg = d.DiffusionConfig(num_timesteps=steps, hidden_size=dm, num_layers=L)
     loop = d.DenoiseLoop(pairs, cfg, cumprod=d.Cumprod.INCLUSIVE, seed=1, kv_cache=None, overlap=False)
     x = torch.randn(M, dm, device=dev, generator=g)
-    loop.sample(x, 2)
-    torch.cuda.synchronize()
-    dist.barrier()
-    t0 = time.perf_counter()
-    out = loop.sample(x, steps)
-    torch.cuda.synchronize()
-    dist.barrier()
-    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    s = float(t.item())
     res = {"workload": f"C5 hidden-dim sharded: {L // 2} TensorParallelPair of int4-g128 d{dm}, seq {M}, "
                        f"{steps} steps, one all-reduce (f32 [{M}, {dm}]) per pair, p_sample, no KV cache",
-           "n_ranks": world, "ms_per_step": round(s / steps * 1e3, 4),
-           "tok_per_s_per_step": round(M / (s / steps), 1), "finite": bool(torch.isfinite(out).all())}
+           "n_ranks": world}
+    for chunks in (1, 4):   # 4: each pair's all-reduce issued per token chunk, overlapping the next GEMM
+        for p in pairs:
+            p.chunks = chunks
+        loop.sample(x, 2)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        out = loop.sample(x, steps)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        s = float(t.item())
+        key = "" if chunks == 1 else f"_chunks{chunks}"
+        res["ms_per_step" + key] = round(s / steps * 1e3, 4)
+        res["tok_per_s_per_step" + key] = round(M / (s / steps), 1)
+        res["finite" + key] = bool(torch.isfinite(out).all())
     for p in pairs:
         p.a.local.close()
         p.b.local.close()

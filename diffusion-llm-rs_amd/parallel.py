@@ -132,9 +132,11 @@ class TensorParallelPair:
         self.b = RowParallelLinear(WB, bB, bits, group, pg, local_factory=local_factory)
         assert (self.b.k0, self.b.k1) == (self.a.n0, self.a.n1)
 
-    def forward(self, x: torch.Tensor, out_dtype=torch.float16, chunks: int = 1) -> torch.Tensor:
+    chunks = 1   # default token chunking of the all-reduce overlap (callers such as DenoiseLoop pass none)
+
+    def forward(self, x: torch.Tensor, out_dtype=torch.float16, chunks: Optional[int] = None) -> torch.Tensor:
         h = self.a(x, out_dtype=torch.float16)
-        return self.b(h, out_dtype=out_dtype, x_is_shard=True, chunks=chunks)
+        return self.b(h, out_dtype=out_dtype, x_is_shard=True, chunks=self.chunks if chunks is None else chunks)
 
     __call__ = forward
 
