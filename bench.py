@@ -5,11 +5,14 @@ M = 4096 tokens, K = N = 4096, W int4 group-128 (per-column, per-group asymmetri
 X/Y f16 resident in HBM, f16 MFMA with f32 accumulation.  Synthetic data: X ~ N(0,1),
 W ~ 0.02 N(0,1), b = 0 (SimpleDiffusionModel::new, diffuse-llm-rs/src/lib.rs:791-801).
 
-Multi-GPU (--gpus N, launched by torch.distributed.run): token-parallel replicas -- every rank owns
-its own M = 4096 tokens and a replica of the 8 MiB int4 weight (linear layers are per-token, so no
-data-path collective exists); value = total tokens over all ranks / max-over-ranks time
-("scaling": "weak").  The hidden-dim (tensor-parallel) variant with RCCL lives in
-diffusion-llm-rs_amd/parallel.py (see DESIGN.md section Multi-GPU).
+Multi-GPU (--gpus N, launched by torch.distributed.run, one process per GPU): the SAME fixed
+4096-token step is split over the ranks by hidden (output) dimension -- column-parallel, rank r
+owns the group-aligned columns [n0, n1) of W (parallel.ColumnParallelLinear), X replicated --
+so ``value`` = 4096 tokens per step / max-over-ranks step time ("scaling": "strong").  No
+collective on that data path (a Megatron column layer hands its Y slice to the row-parallel
+layer after it); the all-gather of the full Y, for a caller that needs it, is timed separately
+(``with_allgather``).  Token-parallel replicas (each rank its own 4096 tokens) are a side key
+(``replicas``, weak scaling), and config C5 hidden-dim sharded over RCCL is ``denoise_loop_tp``.
 """
 from __future__ import annotations
 
@@ -41,7 +44,7 @@ def parse():
     p.add_argument("--group", type=int, default=128)
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--sweep", action="store_true", help="also print an M-sweep to stderr")
+    p.add_argument("--sweep", action="store_true", help="rank 0 at N = 1: add the local layer's M-sweep (m_sweep) to the JSON line")
     p.add_argument("--tp-steps", type=int, default=10,
                    help="N > 1: steps of the hidden-dim-sharded C5 loop reported as 'denoise_loop_tp' (0 skips)")
     p.add_argument("--no-denoise", action="store_true",
@@ -58,9 +61,11 @@ def algorithmic_bytes(M, K, N, bits, group):
 
 
 def cpu_baseline(K, N, bits, group, M, budget_s):
-    """The oracle's restatement of the reference path (a2 dequant of the group-quantized weight,
-    then f32 x.dot(W) + b, diffuse-llm-rs/src/lib.rs:806-813), single-threaded as the reference's
-    ndarray dot is; timed on a bounded row sample and extrapolated to the M-token step."""
+    """The reference path on the host: a2 dequant of the group-quantized weight (the oracle's C
+    restatement), then the f32 ``x.dot(W) + b`` of diffuse-llm-rs/src/lib.rs:806-813 by a blocked
+    AVX2/FMA sgemm (oracle/dllm_sgemm.c) -- the class of kernel ndarray's ``dot`` runs
+    (matrixmultiply) -- on 1 thread (the reference is single-threaded) over as many of the M rows
+    as the budget allows, and on the job's host-core share over all M rows."""
     from oracle import oracle as orc
     rng = np.random.default_rng(0)
     W = (0.02 * rng.standard_normal((K, N))).astype(np.float32)
@@ -69,34 +74,33 @@ def cpu_baseline(K, N, bits, group, M, budget_s):
     What = orc.dequantize_weights(codes, scales, zps, group)
     t_deq = time.perf_counter() - t0
     b = np.zeros(N, np.float32)
-    rows, t_rows = 4, 0.0
-    X = rng.standard_normal((4, K)).astype(np.float32)
+    X = rng.standard_normal((M, K)).astype(np.float32)
+    orc.sgemm_blocked(X[:64], What, b, nthreads=1)                  # page-in / warm
     t0 = time.perf_counter()
-    orc.linear_forward(X, What, b, nthreads=1)
-    t_rows = time.perf_counter() - t0
-    per_row = t_rows / rows
-    rows = int(max(4, min(M, (budget_s - t_deq) / max(per_row, 1e-9))))
-    X = rng.standard_normal((rows, K)).astype(np.float32)
+    orc.sgemm_blocked(X[:256], What, b, nthreads=1)
+    per_row = (time.perf_counter() - t0) / 256
+    rows = int(max(256, min(M, (budget_s - t_deq) / max(per_row, 1e-9))))
     t0 = time.perf_counter()
-    orc.linear_forward(X, What, b, nthreads=1)
+    orc.sgemm_blocked(X[:rows], What, b, nthreads=1)
     t_rows = time.perf_counter() - t0
     t_step = t_deq + t_rows / rows * M
-    # the same restatement on the host cores of this job's share (the GPU box
-    # gives one GPU 16 CPUs; os.cpu_count() there shows the whole machine), rows split by thread.
+    extrap = "" if rows == M else f", extrapolated from {rows} rows"
+    # the same on the host cores of this job's share (the GPU box gives one GPU
+    # 16 CPUs; os.cpu_count() there shows the whole machine).
     threads = max(1, min(16, os.cpu_count() or 1))
-    rows_mt = int(max(threads, min(M, rows * threads)))
-    Xm = rng.standard_normal((rows_mt, K)).astype(np.float32)
+    orc.sgemm_blocked(X[:256], What, b, nthreads=threads)
     t0 = time.perf_counter()
-    orc.linear_forward(Xm, What, b, nthreads=threads)
-    t_mt = time.perf_counter() - t0
-    t_step_mt = t_deq + t_mt / rows_mt * M
-    all_cores = {"value": M / t_step_mt, "unit": "tok/s", "cores": threads,
-                 "sample": f"same restatement, {threads} threads: {rows_mt} of {M} rows ({t_mt:.2f}s), "
-                           f"step extrapolated to {M} rows = {t_step_mt:.2f}s"}
+    orc.sgemm_blocked(X, What, b, nthreads=threads)
+    t_mt = t_deq + time.perf_counter() - t0
+    gf = 2.0 * M * K * N / 1e9
+    all_cores = {"value": M / t_mt, "unit": "tok/s", "cores": threads,
+                 "sample": f"same path on {threads} threads, all {M} rows: {t_mt:.3f}s per step "
+                           f"({gf / (t_mt - t_deq):.0f} GFLOP/s sgemm)"}
     return {"value": M / t_step, "unit": "tok/s", "cores": 1, "kind": "port",
-            "sample": f"C restatement (oracle/dllm_oracle.c), 1 thread: a2 dequant of the {K}x{N} int{bits} "
-                      f"g{group} weight ({t_deq:.3f}s) + f32 sgemm+bias on {rows} of {M} rows "
-                      f"({t_rows:.2f}s), step time extrapolated to {M} rows = {t_step:.2f}s",
+            "sample": f"1 thread: a2 dequant of the {K}x{N} int{bits} g{group} weight ({t_deq:.3f}s, C restatement) "
+                      f"+ blocked AVX2/FMA sgemm (6x16 micro-tile, KC 256, MC 72; matrixmultiply's class) + bias on "
+                      f"{rows} of {M} rows ({t_rows:.2f}s, {2.0 * rows * K * N / t_rows / 1e9:.0f} GFLOP/s){extrap}; "
+                      f"step {t_step:.3f}s",
             "host_cpu": _cpu_model(), "nproc": os.cpu_count(), "all_cores": all_cores}
 
 
@@ -110,17 +114,20 @@ def _cpu_model():
     return "unknown"
 
 
-def load_pmc_traffic():
-    """Per-launch HBM bytes of the GEMM kernel from the committed rocprofv3 PMC summary
-    (profiles/*_pmc_gemm.json, FETCH_SIZE doubled per the gfx950 note + WRITE_SIZE)."""
-    files = sorted((ROOT / "profiles").glob("*_pmc_gemm.json"))
-    if not files:
-        return None
-    try:
-        d = json.loads(files[-1].read_text())
-        return float(d["hbm_bytes_per_launch"])
-    except Exception:
-        return None
+def load_pmc_traffic(cfg):
+    """Per-launch HBM bytes of the bench GEMM from a committed rocprofv3 PMC record whose recorded
+    config (M, K, N_local, bits, group) equals this run's (profiles/**/pmc_gemm.json written by
+    scripts/pmc_to_json.py: FETCH_SIZE doubled per the gfx950 calibration + WRITE_SIZE).  None when
+    no record matches: the figure is never carried over to another shape."""
+    best = None
+    for f in sorted((ROOT / "profiles").glob("**/pmc_gemm.json")):
+        try:
+            d = json.loads(f.read_text())
+        except Exception:
+            continue
+        if d.get("config") == cfg and "hbm_bytes_per_launch" in d:
+            best = (float(d["hbm_bytes_per_launch"]), str(f.relative_to(ROOT)))
+    return best
 
 
 def denoise_loop(d, torch, dev, steps=50):
@@ -158,46 +165,92 @@ def denoise_loop(d, torch, dev, steps=50):
 
 def denoise_loop_tp(d, torch, dist, dev, world, steps):
     """Config C5 hidden-dim sharded over the job's ranks: 12 int4 layers as 6
-    Megatron pairs (parallel.TensorParallelPair: column shard, row shard, one all-reduce(sum) of the
-    f32 partial [2048, 4096] per pair over RCCL), p_sample after the last pair, no KV cache.
-    Every rank builds the same full weights (seeded) and keeps its shard.  Timed with a barrier and
-    synchronize on both sides, max over ranks."""
+    Megatron pairs (parallel.TensorParallelPair: column shard, row shard, one reduction of the f32
+    partial [2048, 4096] per pair over RCCL), p_sample after the last pair, no KV cache.  Every
+    rank builds the same full weights (seeded) and keeps its shard.  Each reduction mode is timed
+    with a barrier and synchronize on both sides, max over ranks: "allreduce" (f32 all_reduce, then
+    bias + f16 cast) and "rs_ag" (f32 reduce_scatter over token rows, cast on the local rows, f16
+    all_gather: 3/4 of the bytes), each unchunked and with the reduction split into 4 token chunks
+    that overlap the next chunk's GEMM."""
     par = d.parallel
     dm, M, L = 4096, 2048, 12
-    g = torch.Generator(device=dev).manual_seed(99)
-    pairs = []
-    for _ in range(L // 2):
-        WA = (0.5 / 64.0) * torch.randn(dm, dm, device=dev, generator=g)
-        WB = (0.5 / 64.0) * torch.randn(dm, dm, device=dev, generator=g)
-        pairs.append(par.TensorParallelPair(WA, None, WB, None, 4, 128))
-        del WA, WB
-    cfg = d.DiffusionConfig(num_timesteps=steps, hidden_size=dm, num_layers=L)
-    loop = d.DenoiseLoop(pairs, cfg, cumprod=d.Cumprod.INCLUSIVE, seed=1, kv_cache=None, overlap=False)
-    x = torch.randn(M, dm, device=dev, generator=g)
     res = {"workload": f"C5 hidden-dim sharded: {L // 2} TensorParallelPair of int4-g128 d{dm}, seq {M}, "
-                       f"{steps} steps, one all-reduce (f32 [{M}, {dm}]) per pair, p_sample, no KV cache",
+                       f"{steps} steps, one reduction of the f32 [{M}, {dm}] partial per pair, p_sample, no KV cache",
            "n_ranks": world}
-    for chunks in (1, 4):   # 4: each pair's all-reduce issued per token chunk, overlapping the next GEMM
+    for mode in ("allreduce", "rs_ag"):
+        g = torch.Generator(device=dev).manual_seed(99)
+        pairs = []
+        for _ in range(L // 2):
+            WA = (0.5 / 64.0) * torch.randn(dm, dm, device=dev, generator=g)
+            WB = (0.5 / 64.0) * torch.randn(dm, dm, device=dev, generator=g)
+            pairs.append(par.TensorParallelPair(WA, None, WB, None, 4, 128, reduce=mode))
+            del WA, WB
+        cfg = d.DiffusionConfig(num_timesteps=steps, hidden_size=dm, num_layers=L)
+        loop = d.DenoiseLoop(pairs, cfg, cumprod=d.Cumprod.INCLUSIVE, seed=1, kv_cache=None, overlap=False)
+        x = torch.randn(M, dm, device=dev, generator=g)
+        for chunks in (1, 4):   # 4: each pair's reduction issued per token chunk, overlapping the next GEMM
+            for p in pairs:
+                p.chunks = chunks
+            loop.sample(x, 2)
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            out = loop.sample(x, steps)
+            torch.cuda.synchronize()
+            dist.barrier()
+            t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            s = float(t.item())
+            key = f"{mode}_chunks{chunks}"
+            res[key] = {"ms_per_step": round(s / steps * 1e3, 4), "tok_per_s_per_step": round(M / (s / steps), 1),
+                        "finite": bool(torch.isfinite(out).all())}
         for p in pairs:
-            p.chunks = chunks
-        loop.sample(x, 2)
-        torch.cuda.synchronize()
-        dist.barrier()
-        t0 = time.perf_counter()
-        out = loop.sample(x, steps)
-        torch.cuda.synchronize()
-        dist.barrier()
-        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        s = float(t.item())
-        key = "" if chunks == 1 else f"_chunks{chunks}"
-        res["ms_per_step" + key] = round(s / steps * 1e3, 4)
-        res["tok_per_s_per_step" + key] = round(M / (s / steps), 1)
-        res["finite" + key] = bool(torch.isfinite(out).all())
-    for p in pairs:
-        p.a.local.close()
-        p.b.local.close()
+            p.close()
     return res
+
+
+def _timed(fn, steps, stream, torch, dist, world, dev):
+    """``steps`` calls of ``fn`` bracketed by barrier + synchronize; returns (max-over-ranks wall
+    seconds, this rank's HIP-event ms per call on ``stream``)."""
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        fn()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t_wall = time.perf_counter() - t0
+    t = torch.tensor([t_wall], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item()), ev0.elapsed_time(ev1) / steps
+
+
+def m_sweep(lin, K, N, bits, group, torch, dev, stream):
+    """Per-M kernel time of the local layer (HIP events, 20 launches after 5 warm)."""
+    rows = []
+    for m in (1, 16, 64, 256, 1024, 2048, 4096, 8192):
+        xs = torch.randn(m, K, device=dev).half()
+        ys = torch.empty(m, N, dtype=torch.float16, device=dev)
+        for _ in range(5):
+            lin(xs, out=ys)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(20):
+            lin(xs, out=ys)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / 20
+        b = algorithmic_bytes(m, K, N, bits, group)
+        rows.append({"M": m, "us": round(ms * 1e3, 2), "tflops": round(2 * m * N * K / ms / 1e9, 1),
+                     "gbs": round(b / ms / 1e6, 1), "hbm_frac": round(b / ms / 1e6 / PEAK_HBM_GBS, 4)})
+    return rows
 
 
 def main():
@@ -225,88 +278,82 @@ def main():
     d.load_library()
 
     M, K, N = args.M, args.K, args.N
-    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+    gen = torch.Generator(device=dev).manual_seed(1234)       # the same W and X on every rank
     W = 0.02 * torch.randn(K, N, device=dev, generator=gen)
     X = torch.randn(M, K, device=dev, generator=gen).half()
-    lin = d.QuantLinear.from_weight(W, None, args.bits, args.group)
-    del W
-    Y = torch.empty(M, N, dtype=torch.float16, device=dev)
+    col = d.parallel.ColumnParallelLinear(W, None, args.bits, args.group, gather=False)
+    lin = col.local
+    n_local = col.n1 - col.n0
+    Y = torch.empty(M, n_local, dtype=torch.float16, device=dev)
     stream = torch.cuda.current_stream()
+
+    def step():
+        lin(X, out=Y)
 
     t_pre = time.perf_counter()
     while (time.perf_counter() - t_pre) * 1e3 < args.prewarm_ms:
         for _ in range(20):
-            lin(X, out=Y)
+            step()
         torch.cuda.synchronize()
     for _ in range(args.warmup):
-        lin(X, out=Y)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        lin(X, out=Y)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t_wall = time.perf_counter() - t0
-    kernel_ms = ev0.elapsed_time(ev1) / args.steps   # HIP events on the launch stream
-
-    t = torch.tensor([t_wall], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    t_max = float(t.item())
+        step()
+    t_max, kernel_ms = _timed(step, args.steps, stream, torch, dist, world, dev)
     ms_per_step = t_max / args.steps * 1e3
-    tokens = M * world * args.steps
-    value = tokens / t_max
+    value = M * args.steps / t_max
 
-    flops = 2.0 * M * N * K
-    abytes = algorithmic_bytes(M, K, N, args.bits, args.group)
-    achieved_tflops = flops / (kernel_ms * 1e-3) / 1e12
+    flops_local = 2.0 * M * n_local * K
+    abytes_local = algorithmic_bytes(M, K, n_local, args.bits, args.group)
+    achieved_tflops = flops_local / (kernel_ms * 1e-3) / 1e12
+    pmc_cfg = {"M": M, "K": K, "N_local": n_local, "bits": args.bits, "group": args.group}
+    pmc = load_pmc_traffic(pmc_cfg)
     out = {
         "metric": "int4 dequant+GEMM GiB/s & tok/s per denoise step, 4096×4096, 1/2/4/8 GPU",
         "value": round(value, 1), "unit": "tok/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 5), "higher_is_better": True, "scaling": "weak",
+        "ms_per_step": round(ms_per_step, 5), "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "f16 (int4 weights)", "data": "synthetic",
-        "config": {"workload": f"int{args.bits}-g{args.group} dequant+GEMM, M={M} tokens x K={K} x N={N} "
-                               f"per rank (token-parallel replicas)",
+        "config": {"workload": f"int{args.bits}-g{args.group} dequant+GEMM, M={M} tokens x K={K} x N={N}, "
+                               f"N split column-parallel over {world} rank(s) ({n_local} columns on rank 0)",
                    "M": M, "K": K, "N": N, "bits": args.bits, "group": args.group,
-                   "global_batch_tokens": M * world, "parallelism": f"token-replica x{world}"},
-        "gib_per_s": round(abytes / (ms_per_step * 1e-3) / 2**30, 1),
-        "tflops": round(flops / (ms_per_step * 1e-3) / 1e12, 1),
+                   "global_batch_tokens": M, "parallelism": f"column-parallel (hidden dim) x{world}"},
+        "gib_per_s": round(algorithmic_bytes(M, K, N, args.bits, args.group) / (ms_per_step * 1e-3) / 2**30, 1),
+        "tflops": round(2.0 * M * N * K / (ms_per_step * 1e-3) / 1e12, 1),
         "roofline": {"bound": "mfma", "achieved": round(achieved_tflops, 1), "peak": PEAK_F16_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved_tflops / PEAK_F16_TFLOPS, 4),
-                     "traffic": load_pmc_traffic(), "algorithmic_bytes": abytes,
-                     "kernel_ms": round(kernel_ms, 5)},
+                     "traffic": None if pmc is None else pmc[0],
+                     "traffic_source": None if pmc is None else pmc[1],
+                     "algorithmic_bytes": abytes_local, "kernel_ms": round(kernel_ms, 5),
+                     "kernel": f"rank 0's local GEMM, M={M} x K={K} x N={n_local}"},
     }
+    if world > 1:
+        def step_gather():
+            lin(X, out=Y)
+            col.all_gather(Y)
+        for _ in range(2):
+            step_gather()
+        tg, _ = _timed(step_gather, args.steps, stream, torch, dist, world, dev)
+        out["with_allgather"] = {"ms_per_step": round(tg / args.steps * 1e3, 5),
+                                 "value": round(M * args.steps / tg, 1),
+                                 "note": "GEMM + RCCL all_gather of the f16 Y slices into the full [M, N] Y"}
+        full = d.QuantLinear.from_weight(W, None, args.bits, args.group)
+        Yf = torch.empty(M, N, dtype=torch.float16, device=dev)
+        for _ in range(args.warmup):
+            full(X, out=Yf)
+        tr, _ = _timed(lambda: full(X, out=Yf), args.steps, stream, torch, dist, world, dev)
+        out["replicas"] = {"value": round(M * world * args.steps / tr, 1), "scaling": "weak",
+                           "ms_per_step": round(tr / args.steps * 1e3, 5),
+                           "note": f"token-parallel replicas: each rank its own {M} tokens x the full weight"}
+        full.close()
+    del W
     if not args.no_denoise:
         out["denoise_loop"] = denoise_loop(d, torch, dev)
         if world > 1 and args.tp_steps > 0:
             out["denoise_loop_tp"] = denoise_loop_tp(d, torch, dist, dev, world, args.tp_steps)
+    if args.sweep and rank == 0 and world == 1:
+        out["m_sweep"] = m_sweep(lin, K, N, args.bits, args.group, torch, dev, stream)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(K, N, args.bits, args.group, M, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if args.sweep and rank == 0:
-        for m in (1, 16, 64, 256, 1024, 2048, 4096, 8192):
-            xs = torch.randn(m, K, device=dev).half()
-            ys = torch.empty(m, N, dtype=torch.float16, device=dev)
-            for _ in range(5):
-                lin(xs, out=ys)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            for _ in range(20):
-                lin(xs, out=ys)
-            e1.record(stream)
-            torch.cuda.synchronize()
-            ms = e0.elapsed_time(e1) / 20
-            b = algorithmic_bytes(m, K, N, args.bits, args.group)
-            print(json.dumps({"sweep_M": m, "us": round(ms * 1e3, 2), "tflops": round(2 * m * N * K / ms / 1e9, 1),
-                              "gbs": round(b / ms / 1e6, 1)}), file=sys.stderr, flush=True)
     lin.close()
     if world > 1:
         dist.destroy_process_group()

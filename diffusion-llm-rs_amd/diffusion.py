@@ -74,7 +74,7 @@ class DiffusionConfig:
     prefill_bits: int = 8
     decode_bits: int = 4
     min_decode_bits: int = 2
-    progressive_precision: bool = False
+    progressive_precision: bool = True      # QuantizationConfig::default() (lib.rs:96-104)
 
     def create_beta_schedule(self) -> np.ndarray:
         """lib.rs:554-593 -> f32 [num_timesteps] (host)."""
@@ -342,12 +342,22 @@ class KVCacheStore:
 
 
 def progressive_bits(config: DiffusionConfig, num_steps: int, t: int) -> int:
-    """lib.rs:890-897: decode bits interpolated towards min_decode_bits over the decode half (f32
-    arithmetic, `as u8` truncation)."""
-    progress = np.float32(num_steps - t) / np.float32(num_steps // 2)
-    v = np.float32(np.float32(config.decode_bits) * (np.float32(1.0) - progress)) + \
-        np.float32(np.float32(config.min_decode_bits) * progress)
-    return int(min(max(np.float32(v), 0), 255)) if np.isfinite(v) else 0
+    """lib.rs:890-897: decode bits interpolated towards min_decode_bits over the decode half:
+    ``((decode * (1 - p) + min * p) as u8`` with p = (num_steps - t) / (num_steps / 2), every op a
+    rounded f32 op and the saturating ``as u8`` (negative and NaN -> 0, +inf -> 255).
+
+    Past the middle of the decode half the target falls below 1 (with 50 steps: 2 at t = 25,
+    1 for t = 24..13, 0 for t <= 12).  Bits 0 is a defined state in the reference, not its
+    ``assert!`` (quantization.rs:39): ``transition_phase`` and ``update`` only quantize when
+    ``decode_quant_bits > 0`` (lib.rs:230, :262), so the decode copy stays ``None`` and
+    ``get_keys``/``get_values`` hand out the f32 K/V (lib.rs:190-197).  KVCacheEntry does the
+    same; quantize_tensor itself still rejects bits outside 1..=8 (InvalidParams)."""
+    f = np.float32
+    progress = f(f(num_steps - t) / f(num_steps // 2)) if num_steps // 2 else f(np.inf if num_steps > t else np.nan)
+    v = f(f(f(config.decode_bits) * f(f(1.0) - progress)) + f(f(config.min_decode_bits) * progress))
+    if np.isnan(v):
+        return 0
+    return int(min(max(np.trunc(v), 0), 255))
 
 
 class DenoiseLoop:

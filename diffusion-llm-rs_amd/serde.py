@@ -77,8 +77,8 @@ def _json_u8_array(a: np.ndarray) -> str:
 # ---- bincode primitives ----------------------------------------------------------------------------
 
 class _Reader:
-    def __init__(self, b: bytes):
-        self.b, self.i = memoryview(b), 0
+    def __init__(self, b: bytes, strict: bool = False):
+        self.b, self.i, self.strict = memoryview(b), 0, strict
 
     def take(self, n):
         if self.i + n > len(self.b):
@@ -116,7 +116,12 @@ class _Reader:
         return self.take(self.u64()).decode("utf-8")
 
     def done(self):
-        if self.i != len(self.b):
+        """bincode 1.3's ``bincode::deserialize`` (the legacy free function the reference's
+        ``bincode`` error conversion serves, quantization/src/error.rs:44-47) is
+        ``DefaultOptions::new().with_fixint_encoding().allow_trailing_bytes()``: bytes after the
+        value are ignored, not an error.  ``strict=True`` readers reject them (the
+        ``DefaultOptions`` default)."""
+        if self.strict and self.i != len(self.b):
             raise _lib.SerializationError("bincode: trailing bytes")
 
 
@@ -150,8 +155,8 @@ def params_to_bincode(p: QuantizationParams) -> bytes:
     return _b_params(p)
 
 
-def params_from_bincode(b: bytes) -> QuantizationParams:
-    r = _Reader(b)
+def params_from_bincode(b: bytes, strict: bool = False) -> QuantizationParams:
+    r = _Reader(b, strict)
     p = _r_params(r)
     r.done()
     return p
@@ -189,8 +194,8 @@ def qtensor_to_bincode(t: QuantizedTensor) -> bytes:
     return _b_bytes(_host_codes(t)) + _b_usize_vec(t.shape) + _b_params(t.params)
 
 
-def qtensor_from_bincode(b: bytes, device="cuda") -> QuantizedTensor:
-    r = _Reader(b)
+def qtensor_from_bincode(b: bytes, device="cuda", strict: bool = False) -> QuantizedTensor:
+    r = _Reader(b, strict)
     data, shape = r.bytes_vec(), r.usize_vec()
     params = _r_params(r)
     r.done()
@@ -202,12 +207,16 @@ def qtensor_to_json(t: QuantizedTensor) -> str:
     return f'{{"data":{_json_u8_array(_host_codes(t))},"shape":{shape},"params":{_params_json(t.params)}}}'
 
 
+def _u8_array(v) -> np.ndarray:
+    """serde's Vec<u8> visitor: every element an integer in 0..=255, else a data error."""
+    if not isinstance(v, list) or not all(type(e) is int and 0 <= e <= 255 for e in v):
+        raise _lib.SerializationError("json: data must be an array of integers in 0..=255")
+    return np.asarray(v, dtype=np.uint8)
+
+
 def qtensor_from_json(s: str, device="cuda") -> QuantizedTensor:
     o = json.loads(s)
-    data = np.asarray(o["data"], dtype=np.int64)
-    if data.size and (data.min() < 0 or data.max() > 255):
-        raise _lib.SerializationError("json: data element out of u8 range")
-    return QuantizedTensor(torch.from_numpy(data.astype(np.uint8)).to(device), tuple(int(v) for v in o["shape"]),
+    return QuantizedTensor(torch.from_numpy(_u8_array(o["data"])).to(device), tuple(int(v) for v in o["shape"]),
                            _params_from_obj(o["params"]))
 
 
@@ -230,8 +239,8 @@ class PrefillCompressedVector:
                                                                 float(F32(self.quant_zero_point))))
 
     @classmethod
-    def from_bincode(cls, b: bytes) -> "PrefillCompressedVector":
-        r = _Reader(b)
+    def from_bincode(cls, b: bytes, strict: bool = False) -> "PrefillCompressedVector":
+        r = _Reader(b, strict)
         v = cls(r.string(), r.bytes_vec(), r.u8(), r.usize_vec(), float(r.f32()), float(r.f32()))
         r.done()
         return v
@@ -246,7 +255,10 @@ class PrefillCompressedVector:
     def from_json(cls, s: str) -> "PrefillCompressedVector":
         o = json.loads(s)
         f = (lambda v: float(F32(float("nan") if v is None else float(v))))
-        return cls(o["id"], np.asarray(o["data"], np.uint8), int(o["bits"]), [int(v) for v in o["original_shape"]],
+        bits = int(o["bits"])
+        if not 0 <= bits <= 255:
+            raise _lib.SerializationError("json: bits out of u8 range")
+        return cls(o["id"], _u8_array(o["data"]), bits, [int(v) for v in o["original_shape"]],
                    f(o["quant_scale"]), f(o["quant_zero_point"]))
 
 
@@ -257,7 +269,7 @@ def compressed_vector_records(x: torch.Tensor, bits: int, ids: Optional[List[str
     codes, scales, zps = compress_vectors(x, bits)
     codes, scales, zps = codes.cpu().numpy(), scales.cpu().numpy(), zps.cpu().numpy()
     rows = codes.shape[0]
-    shape = [int(s) for s in x.shape[1:]] or [int(codes.shape[1])]
+    shape = [int(codes.shape[1])]       # vec![vector.len()] (prefill_kv.rs:117): the row's length
     ids = ids or [str(i) for i in range(rows)]
     return [PrefillCompressedVector(ids[i], codes[i].copy(), int(bits), shape, float(scales[i]), float(zps[i]))
             for i in range(rows)]

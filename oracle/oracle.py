@@ -19,7 +19,7 @@ _lib = None
 
 
 def build(force: bool = False) -> Path:
-    srcs = [HERE / "dllm_oracle.c", HERE / "dllm_oracle_diffusion.c", HERE / "dllm_oracle.h"]
+    srcs = [HERE / "dllm_oracle.c", HERE / "dllm_oracle_diffusion.c", HERE / "dllm_oracle.h", HERE / "dllm_sgemm.c"]
     newest = max(p.stat().st_mtime for p in srcs)
     if force or not LIB_PATH.exists() or LIB_PATH.stat().st_mtime < newest:
         subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
@@ -49,6 +49,7 @@ def lib():
             "orc_quantize_weights": (C.c_int, [P, S, S, U8, S, P, P, P]),
             "orc_dequantize_weights": (None, [P, P, P, S, S, S, P]),
             "orc_linear_forward": (None, [P, S, S, P, S, P, P, C.c_int]),
+            "orc_sgemm_blocked": (C.c_int, [P, S, S, P, S, P, P, C.c_int]),
             "orc_attention": (None, [P, P, P, S, S, S, P, S, C.c_int]),
             "orc_beta_schedule": (C.c_int, [C.c_int, S, F, F, P]),
             "orc_alpha_bars": (C.c_int, [P, S, C.c_int, P, P]),
@@ -195,6 +196,36 @@ def linear_forward(X, W, bias=None, nthreads=1):
     return Y
 
 
+def sgemm_blocked(X, W, bias=None, nthreads=1):
+    """Y = X . W + bias by the blocked AVX2/FMA GEMM (dllm_sgemm.c): the CPU baseline's GEMM, of
+    the class ndarray's dot runs (matrixmultiply).  Not a parity restatement (FMA, blocked order)."""
+    X = np.ascontiguousarray(X, np.float32)
+    W = np.ascontiguousarray(W, np.float32)
+    M, K = X.shape
+    N = W.shape[1]
+    Y = np.empty((M, N), np.float32)
+    b = None if bias is None else np.ascontiguousarray(bias, np.float32)
+    if lib().orc_sgemm_blocked(_p(X), M, K, _p(W), N, None if b is None else _p(b), _p(Y), nthreads) != 0:
+        raise RuntimeError("orc_sgemm_blocked: no AVX2/FMA on this host or allocation failed")
+    return Y
+
+
+def attention_rows(Qsel, K, V):
+    """f64 SDPA softmax(q K^T / sqrt(D)) V (bidirectional, the a9 consumer's definition) for a
+    selection of query rows Qsel [R, H, D] against all keys K, V [S, H, D]: the same math as
+    orc_attention, for rows sampled across a long sequence."""
+    Qs = np.asarray(Qsel, np.float64)
+    R, H, D = Qs.shape
+    out = np.empty((R, H, D), np.float64)
+    inv = 1.0 / np.sqrt(D)
+    for h in range(H):
+        s = (Qs[:, h, :] @ np.asarray(K[:, h, :], np.float64).T) * inv
+        s -= s.max(axis=1, keepdims=True)
+        p = np.exp(s)
+        out[:, h, :] = (p @ np.asarray(V[:, h, :], np.float64)) / p.sum(axis=1, keepdims=True)
+    return out
+
+
 def attention(Q, K, V, q_rows=None, nthreads=None):
     Q, K, V = (np.ascontiguousarray(a, np.float32) for a in (Q, K, V))
     S, H, D = Q.shape
@@ -292,3 +323,80 @@ class AdaptiveQuantizer:
         out = np.zeros(x.size, np.uint8)
         _check(lib().orc_adaptive_quantize(_p(x), x.size, self.bits, float(s), float(z), _p(out)))
         return out, s, z
+
+
+# ---- 8f rank 2: phase-aware KV cache + progressive precision (diffuse-llm-rs/src/lib.rs) --------
+
+def progressive_bits(decode_bits: int, min_decode_bits: int, num_steps: int, t: int) -> int:
+    """lib.rs:890-897: progress = (num_steps - t) as f32 / (num_steps / 2) as f32;
+    target = (decode * (1 - progress) + min * progress) as u8 -- f32 ops, each rounded, and the
+    saturating `as u8` (negative -> 0, NaN -> 0, truncation toward zero)."""
+    f = np.float32
+    progress = f(f(num_steps - t) / f(num_steps // 2))
+    v = f(f(f(decode_bits) * f(f(1.0) - progress)) + f(f(min_decode_bits) * progress))
+    if not np.isfinite(v):
+        return 0 if np.isnan(v) else (255 if v > 0 else 0)
+    return int(min(max(int(np.trunc(v)), 0), 255))
+
+
+class KVCacheEntryRef:
+    """Oracle restatement of KVCacheEntry (lib.rs:121-313) over host f32 K/V and the C oracle's
+    quantize_tensor / dequantize_tensor (QuantizedKVCacheEntry::new quantizes K and V per tensor,
+    quantization.rs:140-157): an Option<(codes, scale, zp)> per tensor and phase."""
+
+    def __init__(self, keys, values, prefill_bits, decode_bits):
+        self.keys = np.ascontiguousarray(keys, np.float32)
+        self.values = np.ascontiguousarray(values, np.float32)
+        self.prefill_quant_bits, self.decode_quant_bits = int(prefill_bits), int(decode_bits)
+        self.prefill_quantized = self._q(prefill_bits) if prefill_bits > 0 else None    # :145-153
+        self.decode_quantized = self._q(decode_bits) if decode_bits > 0 else None       # :155-163
+        self.is_prefill_phase = True
+
+    def _q(self, bits):
+        return (quantize_tensor(self.keys, bits), quantize_tensor(self.values, bits))
+
+    def _get(self, which):                                                              # :178-208
+        q = self.prefill_quantized if self.is_prefill_phase else self.decode_quantized
+        src = self.keys if which == 0 else self.values
+        if q is None:
+            return src.copy()
+        return dequantize_tensor(*q[which]).reshape(src.shape)
+
+    def get_keys(self):
+        return self._get(0)
+
+    def get_values(self):
+        return self._get(1)
+
+    def set_phase(self, is_prefill):                                                    # :221-239
+        if self.is_prefill_phase == is_prefill:
+            return
+        self.is_prefill_phase = is_prefill
+        if not is_prefill and self.decode_quant_bits > 0 and self.decode_quantized is None:
+            self.decode_quantized = self._q(self.decode_quant_bits)
+
+    def update(self, keys, values):                                                     # :246-276
+        self.keys = np.ascontiguousarray(keys, np.float32)
+        self.values = np.ascontiguousarray(values, np.float32)
+        if self.prefill_quant_bits > 0:
+            self.prefill_quantized = self._q(self.prefill_quant_bits)
+        if self.decode_quant_bits > 0:
+            self.decode_quantized = self._q(self.decode_quant_bits)
+
+
+def sample_kv_step(entry: KVCacheEntryRef, t: int, num_steps: int, decode_bits: int, min_decode_bits: int,
+                   progressive: bool = True, phase_aware: bool = True):
+    """The cache half of one DiffuseLLM::sample iteration (lib.rs:884-918) with the simple model's
+    pass-through update_kv_cache (:826-835): phase switch, progressive decode bits, the K/V that
+    forward_with_cache receives, then the re-quantizing update.  Returns (keys, values) given."""
+    is_prefill = t > num_steps // 2                                                     # :886
+    entry.set_phase(is_prefill)
+    if phase_aware and progressive and not is_prefill:                                   # :890-903
+        tb = progressive_bits(decode_bits, min_decode_bits, num_steps, t)
+        if tb != entry.decode_quant_bits:
+            entry.decode_quant_bits = tb
+            entry.decode_quantized = None
+    new_k, new_v = entry.keys, entry.values                                             # :907
+    k, v = entry.get_keys(), entry.get_values()                                         # :913-914
+    entry.update(new_k, new_v)                                                          # :918
+    return k, v

@@ -150,3 +150,39 @@ def test_product_coeff_errors(lib):
     assert lib.dllm_p_sample_coeffs(_ptr(b), 4, 7, 0, _ptr(t), 2, _ptr(coef), C.byref(flag)) == 1   # bad cumprod
     assert lib.dllm_beta_schedule(9, 4, 0.1, 0.2, _ptr(b)) == 1
     assert lib.dllm_p_sample_coeffs(_ptr(b), 4, 0, 0, _ptr(t), 2, _ptr(coef), C.byref(flag)) == 0 and flag.value == 0
+
+
+def test_progressive_bits_sequence(orc):
+    """Progressive decode precision (lib.rs:890-903, on by default: QuantizationConfig::default,
+    lib.rs:96-104) for the C5 schedule of 50 steps: prefill while t > 25, then the target width is
+    2 at t = 25, 1 for t = 24..13 and 0 for t <= 12 (the saturating `as u8` of a negative f32)."""
+    seq = [orc.progressive_bits(4, 2, 50, t) for t in range(25, -1, -1)]
+    assert seq == [2] + [1] * 12 + [0] * 13
+
+
+def test_progressive_bits_product_matches_oracle(dllm, orc):
+    """The product's host-side target-width arithmetic equals the oracle's restatement for every
+    (num_steps, t) up to 80 steps and several (decode, min) widths, including num_steps = 1
+    (progress = 1/0 = inf, so the f32 expression is NaN -> 0)."""
+    for ns in range(1, 81):
+        for t in range(ns):
+            for db, mb in ((4, 2), (8, 1), (3, 3), (2, 4), (8, 0)):
+                cfg = dllm.DiffusionConfig(decode_bits=db, min_decode_bits=mb)
+                assert dllm.diffusion.progressive_bits(cfg, ns, t) == orc.progressive_bits(db, mb, ns, t), (ns, t, db, mb)
+    assert dllm.DiffusionConfig().progressive_precision is True
+
+
+def test_kv_cache_ref_zero_bits_hands_out_f32(orc):
+    """The oracle's KVCacheEntry restatement: once progressive precision drives decode bits to 0
+    the decode copy is None and get_keys returns the f32 keys (lib.rs:190-197); no
+    quantize_tensor(.., 0) is ever made (the `> 0` guards of lib.rs:230, :262)."""
+    rng = np.random.default_rng(2)
+    K = rng.standard_normal((1, 16, 32)).astype(np.float32)
+    e = orc.KVCacheEntryRef(K, 2 * K, 8, 4)
+    widths = []
+    for t in range(9, -1, -1):
+        k, v = orc.sample_kv_step(e, t, 10, 4, 2)
+        widths.append(e.decode_quant_bits if not e.is_prefill_phase else e.prefill_quant_bits)
+        if not e.is_prefill_phase and e.decode_quant_bits == 0:
+            assert np.array_equal(k, K) and np.array_equal(v, 2 * K)
+    assert widths == [8, 8, 8, 8, 2, 1, 1, 0, 0, 0]

@@ -1,0 +1,149 @@
+"""GPU parity of the hidden-dim-sharded linear layer (SURVEY.md 8e, config C5 sharded): the HIP
+GEMM composed with the partition logic of diffusion-llm-rs_amd/parallel.py, G = 2/4/8 ranks
+emulated in one process (``shard=(G, r)`` builds rank r's shard; collectives are replaced by
+their definition: concatenation for the column all_gather, an f32 sum for the row reduction).
+
+Shapes are the sharded C5 / bench shapes: M = 2048 or 4096 tokens, d = 4096, column shards of
+N = 2048/1024/512 and row shards of K = 2048/1024/512 -- each selects its own tile / split-K
+policy, so every shard shape runs through the HIP kernels it will use on G GPUs.
+
+* Exact-integer data (W with integer values in [-8, 7] whose every (column, group) holds both -8
+  and 7, so quantize_tensor gives scale 1, zp 8 and W^ = W exactly; X integers in [-3, 3]):
+  every partial sum is exact in f32, so shard outputs must equal the unsharded layer BIT FOR BIT
+  whatever tiling or K-split each shard uses.
+* Random data: shard weight quantization is bit-identical to the unsharded columns/groups, and
+  the composed outputs are within 1e-3 (relative Frobenius) of torch f32 on the
+  oracle-dequantized weights (reference: x.dot(W) + b, diffuse-llm-rs/src/lib.rs:806-813).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REL_TOL = 1e-3
+D = 4096
+
+
+@pytest.fixture(scope="module")
+def torch(cuda):
+    import torch as t
+    return t
+
+
+def _exact_weight(torch, K, N, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    W = torch.randint(-8, 8, (K, N), device="cuda", generator=g).float()
+    W[0::128, :] = -8.0      # every (column, group) holds both extremes -> scale 1, zp 8
+    W[1::128, :] = 7.0
+    return W
+
+
+def _exact_x(torch, M, K, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    return torch.randint(-3, 4, (M, K), device="cuda", generator=g).half()
+
+
+def _dequantized(lin, orc):
+    """The layer's exported codes dequantized by the oracle (a2 per group) -> torch f32 on the GPU."""
+    import torch as t
+    codes, s, z = lin.export()
+    cd = orc.unpack_bits(codes.cpu().numpy(), lin.K * lin.N, lin.bits).reshape(lin.K, lin.N)
+    return t.from_numpy(orc.dequantize_weights(cd, s.cpu().numpy(), z.cpu().numpy(), lin.group)).cuda()
+
+
+def _rel(a, b):
+    return ((a.double() - b.double()).norm() / b.double().norm()).item()
+
+
+@pytest.mark.parametrize("G", [2, 4, 8])
+@pytest.mark.parametrize("M", [2048, 4096])
+def test_column_shards_exact_integer_bit_equal(dllm, torch, G, M):
+    par = dllm.parallel
+    W = _exact_weight(torch, D, D, 11)
+    X = _exact_x(torch, M, D, 12)
+    full = dllm.QuantLinear.from_weight(W, None, 4, 128)
+    Y = full(X, out_dtype=torch.float32)
+    ref = (X.double() @ W.double()).float()
+    assert torch.equal(Y, ref)                                  # exact data: W^ = W, sums exact
+    parts = []
+    for r in range(G):
+        col = par.ColumnParallelLinear(W, None, 4, 128, shard=(G, r))
+        assert col.n1 - col.n0 == D // G
+        parts.append(col(X, out_dtype=torch.float32))
+        col.local.close()
+    assert torch.equal(torch.cat(parts, dim=1), Y)
+    full.close()
+
+
+@pytest.mark.parametrize("G", [2, 4, 8])
+def test_row_shards_exact_integer_partials_sum(dllm, torch, G):
+    par = dllm.parallel
+    M = 2048
+    W = _exact_weight(torch, D, D, 13)
+    X = _exact_x(torch, M, D, 14)
+    ref = (X.double() @ W.double()).float()
+    tot = torch.zeros(M, D, device="cuda")
+    for r in range(G):
+        row = par.RowParallelLinear(W, None, 4, 128, shard=(G, r))
+        assert row.k1 - row.k0 == D // G
+        tot += row.partial(X)
+        row.local.close()
+    assert torch.equal(tot, ref)
+
+
+@pytest.mark.parametrize("G", [2, 4, 8])
+def test_tensor_parallel_pair_random_vs_f32(dllm, torch, orc, G):
+    """Megatron pair at the C5 shape (M = 2048, d = 4096, 0.5/sqrt(d) N(0,1) weights, bias on B):
+    shard codes/scales/zps bit-identical to the unsharded layers' columns (A) and groups (B); the
+    f32 sum of the G partials (+ bias) within 1e-3 of torch f32 on the oracle-dequantized weights
+    with the hidden activation rounded to f16 as the GPU hands it between the layers; the
+    reduce-scatter form (f16 output) is the RNE of that sum."""
+    par = dllm.parallel
+    M = 2048
+    g = torch.Generator(device="cuda").manual_seed(G)
+    WA = (0.5 / 64) * torch.randn(D, D, device="cuda", generator=g)
+    WB = (0.5 / 64) * torch.randn(D, D, device="cuda", generator=g)
+    bB = 0.1 * torch.randn(D, device="cuda", generator=g)
+    X = torch.randn(M, D, device="cuda", generator=g).half()
+    fa = dllm.QuantLinear.from_weight(WA, None, 4, 128)
+    fb = dllm.QuantLinear.from_weight(WB, bB, 4, 128)
+    ca, sa, za = fa.export()
+    cb, sb, zb = fb.export()
+    ca = orc.unpack_bits(ca.cpu().numpy(), D * D, 4).reshape(D, D)
+    cb = orc.unpack_bits(cb.cpu().numpy(), D * D, 4).reshape(D, D)
+    WAh, WBh = _dequantized(fa, orc), _dequantized(fb, orc)
+    H = (X.float() @ WAh).half().float()
+    Z = H @ WBh + bB[None, :]
+    tot = torch.zeros(M, D, device="cuda")
+    for r in range(G):
+        pair = par.TensorParallelPair(WA, None, WB, bB, 4, 128, shard=(G, r))
+        n0, n1 = pair.a.n0, pair.a.n1
+        c, s, z = pair.a.local.export()
+        assert np.array_equal(orc.unpack_bits(c.cpu().numpy(), D * (n1 - n0), 4).reshape(D, n1 - n0), ca[:, n0:n1])
+        assert torch.equal(s, sa[:, n0:n1]) and torch.equal(z, za[:, n0:n1])
+        c, s, z = pair.b.local.export()
+        k0, k1 = pair.b.k0, pair.b.k1
+        assert np.array_equal(orc.unpack_bits(c.cpu().numpy(), (k1 - k0) * D, 4).reshape(k1 - k0, D), cb[k0:k1])
+        assert torch.equal(s, sb[k0 // 128:k1 // 128]) and torch.equal(z, zb[k0 // 128:k1 // 128])
+        tot += pair.partial(X)
+        pair.close()
+    Y = tot + bB[None, :]
+    assert _rel(Y, Z) <= REL_TOL, _rel(Y, Z)
+    fa.close()
+    fb.close()
+
+
+@pytest.mark.parametrize("G", [1, 2, 4, 8])
+def test_bench_column_shard_random_vs_f32(dllm, torch, orc, G):
+    """The bench's strong-scaling shard (M = 4096 tokens, int4 g128 0.02 N(0,1) weights, rank 0's
+    N = 4096/G columns, f16 in/out) within 1e-3 of torch f32 on the oracle-dequantized shard."""
+    par = dllm.parallel
+    g = torch.Generator(device="cuda").manual_seed(1234)
+    W = 0.02 * torch.randn(D, D, device="cuda", generator=g)
+    X = torch.randn(4096, D, device="cuda", generator=g).half()
+    for r in sorted({0, G - 1}):
+        col = par.ColumnParallelLinear(W, None, 4, 128, shard=(G, r))
+        Y = col(X, out_dtype=torch.float16)
+        ref = X.float() @ _dequantized(col.local, orc)
+        assert _rel(Y.float(), ref) <= REL_TOL, (r, _rel(Y.float(), ref))
+        col.local.close()

@@ -534,12 +534,24 @@ def test_kv_attention_peaked_softmax(dllm, torch, orc):
     assert rel_err(O[5], Oref[5]) <= REL_TOL
 
 
+def _tile_rows(S, tile=256, extra=(), stride=37):
+    """Query rows that touch every ``tile``-query workgroup of the attention kernel: each tile's
+    first and last row and one pseudo-random interior row, plus ``extra``."""
+    rows = set(r for r in extra if 0 <= r < S)
+    for t0 in range(0, S, tile):
+        t1 = min(S, t0 + tile)
+        rows.update({t0, t1 - 1, t0 + (t0 // tile * stride) % (t1 - t0)})
+    return np.array(sorted(rows))
+
+
 def test_kv_quantize_attention_config4_full_size(dllm, torch, orc):
     """Config C4 at its full size (K, V, Q [8192, 32, 128]): the int4 per-tensor KV quantization
     is bit-exact against the C oracle on all 33.5 M elements of each tensor (packed codes and
-    params), and the dequant-attention of the first 64 queries of every head (all 8192 keys)
-    is within REL_TOL of the oracle's f64 SDPA on the oracle-dequantized K and V."""
-    S, H, D, rows = 8192, 32, 128, 64
+    params), and the dequant-attention is within REL_TOL of the oracle's f64 SDPA on the
+    oracle-dequantized K and V, on query rows from EVERY 256-query tile of every head (first,
+    last and one interior row of each of the 32 tiles, plus rows 0, 255, 256, 4095, 4096, 8191),
+    against all 8192 keys."""
+    S, H, D = 8192, 32, 128
     rng = np.random.default_rng(84)
     K = rng.standard_normal((S, H, D), dtype=np.float32)
     V = rng.standard_normal((S, H, D), dtype=np.float32)
@@ -551,9 +563,37 @@ def test_kv_quantize_attention_config4_full_size(dllm, torch, orc):
         assert np.array_equal(host(t.data), orc.pack_bits(rq, 4))
         assert same_bits(host(t.params), np.array([rs, rz], np.float32))
         deq.append(orc.dequantize_tensor(rq, rs, rz).reshape(S, H, D))
-    O = host(dllm.kv_attention(dev(torch, Q), e.keys, e.values)[:rows].float())
-    Oref = orc.attention(Q.astype(np.float32), deq[0], deq[1], q_rows=rows)
-    assert rel_err(O, Oref) <= REL_TOL, rel_err(O, Oref)
+    rows = _tile_rows(S, extra=(0, 255, 256, 4095, 4096, 8191))
+    assert len(set(rows // 256)) == S // 256
+    O = host(dllm.kv_attention(dev(torch, Q), e.keys, e.values).float())[rows]
+    Oref = orc.attention_rows(Q.astype(np.float32)[rows], deq[0], deq[1])
+    for h in range(H):
+        assert rel_err(O[:, h], Oref[:, h]) <= REL_TOL, (h, rel_err(O[:, h], Oref[:, h]))
+    for i in range(len(rows)):   # every sampled row of every tile, all heads
+        assert rel_err(O[i], Oref[i]) <= REL_TOL, (rows[i], rel_err(O[i], Oref[i]))
+
+
+@pytest.mark.parametrize("S,H,bits", [(8003, 4, 4), (4160, 3, 8), (65, 2, 4)])
+def test_kv_attention_ragged_full_tiles(dllm, torch, orc, S, H, bits):
+    """Ragged S: a partial last 256-query tile AND a partial last 64-key block (8003 = 31*256 + 67
+    = 125*64 + 3; 4160 = 16*256 + 64 with whole key blocks; 65 = one tile, two key blocks); rows
+    from every query tile, including every row of the partial last tile, vs the f64 oracle."""
+    rng = np.random.default_rng(S + H)
+    D = 128
+    K = rng.standard_normal((S, H, D), dtype=np.float32)
+    V = (rng.standard_normal((S, H, D), dtype=np.float32) * 1.5 - 0.25).astype(np.float32)
+    Q = rng.standard_normal((S, H, D), dtype=np.float32).astype(np.float16)
+    kq = dllm.QuantizedTensor.quantize(dev(torch, K), bits, packed=True)
+    vq = dllm.QuantizedTensor.quantize(dev(torch, V), bits, packed=True)
+    Kh = orc.dequantize_tensor(*orc.quantize_tensor(K.ravel(), bits)).reshape(S, H, D)
+    Vh = orc.dequantize_tensor(*orc.quantize_tensor(V.ravel(), bits)).reshape(S, H, D)
+    last = (S - 1) // 256 * 256
+    rows = np.union1d(_tile_rows(S), np.arange(last, S))
+    O = host(dllm.kv_attention(dev(torch, Q), kq, vq).float())[rows]
+    Oref = orc.attention_rows(Q.astype(np.float32)[rows], Kh, Vh)
+    assert np.isfinite(O).all()
+    for i in range(len(rows)):
+        assert rel_err(O[i], Oref[i]) <= REL_TOL, (rows[i], rel_err(O[i], Oref[i]))
 
 
 @pytest.mark.parametrize("S,H,bits", [(512, 2, 4), (333, 3, 8), (8192, 2, 4)])

@@ -209,3 +209,14 @@ def test_oracle_attention_softmax_identity(orc):
         V[j, :, j] = 1.0
     O = orc.attention(Q, K, V, nthreads=1)
     assert np.allclose(O[:, :, :S], 1.0 / S) and np.allclose(O[:, :, S:], 0.0)
+
+
+def test_attention_rows_matches_c_oracle(orc):
+    """The row-sampled f64 SDPA checker (oracle.attention_rows) agrees with the C oracle's
+    orc_attention on the same rows."""
+    rng = np.random.default_rng(9)
+    S, H, D = 200, 3, 128
+    Q, K, V = (rng.standard_normal((S, H, D)).astype(np.float32) for _ in range(3))
+    full = orc.attention(Q, K, V)
+    rows = np.array([0, 7, 63, 64, 199])
+    np.testing.assert_allclose(orc.attention_rows(Q[rows], K, V), full[rows], rtol=0, atol=1e-6)

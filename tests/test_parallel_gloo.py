@@ -70,6 +70,13 @@ def _worker(rank, world, port, outdir):
     res["pair_y"] = pair(X, out_dtype=torch.float32).numpy()
     res["pair_y_chunked"] = pair(X, out_dtype=torch.float32, chunks=3).numpy()
     res["row_y_chunked"] = row(X, out_dtype=torch.float32, chunks=5).numpy()
+    row_rs = par.RowParallelLinear(WA, bA, 4, 128, local_factory=OracleLinear, reduce="rs_ag")
+    res["row_rs_y"] = row_rs(X, out_dtype=torch.float32).numpy()
+    res["row_rs_y_odd"] = row_rs(X[:23], out_dtype=torch.float32).numpy()       # padded scatter
+    res["row_rs_y_chunked"] = row_rs(X, out_dtype=torch.float32, chunks=3).numpy()
+    res["row_rs_y16"] = row_rs(X, out_dtype=torch.float16).float().numpy()
+    pair_rs = par.TensorParallelPair(WA, bA, WB, bB, 4, 128, local_factory=OracleLinear, reduce="rs_ag")
+    res["pair_rs_y"] = pair_rs(X, out_dtype=torch.float32, chunks=2).numpy()
     tok = par.TokenParallelLinear(WA, bA, 4, 128, local_factory=OracleLinear)
     m0, m1 = tok.token_range(M)
     res["tok_y"], res["tok_range"] = tok(X[m0:m1], out_dtype=torch.float32).numpy(), np.array([m0, m1])
@@ -137,3 +144,38 @@ def test_chunked_allreduce_overlap_is_identical(gloo_results):
     for r in gloo_results:
         assert np.array_equal(r["row_y_chunked"], r["row_y"])
         assert np.array_equal(r["pair_y_chunked"], r["pair_y"])
+
+
+def test_reduce_scatter_all_gather_mode(gloo_results):
+    """reduce="rs_ag" (f32 reduce_scatter over token rows, bias and cast on the local rows, then an
+    all_gather of the cast rows) gives the all-reduce result: at world size 2 the f32 sum of two
+    partials is order-free, so bit for bit, also with padded (M = 23) and chunked scatters; the
+    f16 output is the RNE of the f32 one; the pair equals the all-reduce pair."""
+    for r in gloo_results:
+        assert np.array_equal(r["row_rs_y"], r["row_y"])
+        assert np.array_equal(r["row_rs_y_odd"], r["row_y"][:23])
+        assert np.array_equal(r["row_rs_y_chunked"], r["row_y"])
+        assert np.array_equal(r["row_rs_y16"], r["row_y"].astype(np.float16).astype(np.float32))
+        assert np.array_equal(r["pair_rs_y"], r["pair_y"])
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_shard_emulation_partials_sum_to_unsharded(world):
+    """``shard=(world, rank)`` (one process, no collective) builds each rank's shard: column
+    slices concatenate to the unsharded output exactly, and the row-parallel f32 partials sum to
+    it within the f32 reduction-order tolerance -- the composition the GPU tests run on HIP."""
+    sys.path.insert(0, str(ROOT))
+    import __graft_entry__ as g
+    par = g.load_package().parallel
+    WA, WB, bA, bB, X = _reference()
+    lin = OracleLinear(torch.from_numpy(WA), torch.from_numpy(bA), 4, 128)
+    Y = lin(torch.from_numpy(X)).numpy()
+    Xt = torch.from_numpy(X)
+    cols = [par.ColumnParallelLinear(torch.from_numpy(WA), torch.from_numpy(bA), 4, 128, local_factory=OracleLinear,
+                                     shard=(world, r)) for r in range(world)]
+    assert [c.n0 for c in cols[1:]] == [c.n1 for c in cols[:-1]] and cols[-1].n1 == WA.shape[1]
+    np.testing.assert_array_equal(np.concatenate([c(Xt, out_dtype=torch.float32).numpy() for c in cols], 1), Y)
+    rows = [par.RowParallelLinear(torch.from_numpy(WA), torch.from_numpy(bA), 4, 128, local_factory=OracleLinear,
+                                  shard=(world, r)) for r in range(world)]
+    tot = sum(r_.partial(Xt).numpy().astype(np.float64) for r_ in rows) + bA[None, :]
+    np.testing.assert_allclose(tot, Y, rtol=0, atol=1e-5)

@@ -46,8 +46,10 @@ def test_params_bincode_layout(sd):
     assert sd.serde.params_from_bincode(b) == p and sd.serde.params_from_bincode(b2) == q
     with pytest.raises(sd.SerializationError):
         sd.serde.params_from_bincode(b2[:-1])
+    # bincode 1.3's deserialize (legacy options) allows trailing bytes; strict readers reject them
+    assert sd.serde.params_from_bincode(b + b"\x00\x07") == p
     with pytest.raises(sd.SerializationError):
-        sd.serde.params_from_bincode(b + b"\x00")
+        sd.serde.params_from_bincode(b + b"\x00", strict=True)
 
 
 def test_params_json(sd):
@@ -94,3 +96,14 @@ def test_compressed_vector_record(sd):
                  '"quant_scale":0.06666667,"quant_zero_point":-0.5}')
     r3 = sd.serde.PrefillCompressedVector.from_json(s)
     assert np.float32(r3.quant_scale) == np.float32(0.0666666701)
+
+
+def test_compressed_vector_json_u8_range_and_shape(sd):
+    """from_json rejects codes outside u8 (serde's Vec<u8> visitor) with SerializationError, not an
+    OverflowError or a silent wrap; a 3-D input row's record has original_shape = [row length]
+    (vec![vector.len()], prefill_kv.rs:117)."""
+    good = ('{"id":"a","data":[1,255],"bits":4,"original_shape":[2],"quant_scale":0.5,"quant_zero_point":0.0}')
+    assert list(sd.serde.PrefillCompressedVector.from_json(good).data) == [1, 255]
+    for bad in ('[1,256]', '[-1,2]', '[1.5,2]', '[[1],[2]]'):
+        with pytest.raises(sd.SerializationError):
+            sd.serde.PrefillCompressedVector.from_json(good.replace('[1,255]', bad))
