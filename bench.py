@@ -2,8 +2,11 @@
 
 Workload (BASELINE.json metric, north_star shape): one step = Y[M][N] = X[M][K] . W^[K][N] + b with
 M = 4096 tokens, K = N = 4096, W int4 group-128 (per-column, per-group asymmetric quantize_tensor),
-X/Y f16 resident in HBM, f16 MFMA with f32 accumulation.  Synthetic data: X ~ N(0,1),
-W ~ 0.02 N(0,1), b = 0 (SimpleDiffusionModel::new, diffuse-llm-rs/src/lib.rs:791-801).
+X/Y f16 resident in HBM, f16 MFMA with f32 accumulation, the library's default precision
+(DLLM_PRECISION_EXACT: the MFMA consumes the exact integer q - zp, the f32 group scale is applied
+to each group's partial sum).  The rounded-weight mode (DLLM_PRECISION_F16W) is timed beside it
+as ``f16_weights``.  Synthetic data: X ~ N(0,1), W ~ 0.02 N(0,1), b = 0 (SimpleDiffusionModel::new,
+diffuse-llm-rs/src/lib.rs:791-801).
 
 Multi-GPU (--gpus N, launched by torch.distributed.run, one process per GPU): the SAME fixed
 4096-token step is split over the ranks by hidden (output) dimension -- column-parallel, rank r
@@ -310,7 +313,8 @@ def main():
         "metric": "int4 dequant+GEMM GiB/s & tok/s per denoise step, 4096×4096, 1/2/4/8 GPU",
         "value": round(value, 1), "unit": "tok/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 5), "higher_is_better": True, "scaling": "strong",
-        "vs_baseline": None, "dtype": "f16 (int4 weights)", "data": "synthetic",
+        "vs_baseline": None, "dtype": "f16 X x exact int4 weights (f32 group scales), f32 accumulate",
+        "data": "synthetic",
         "config": {"workload": f"int{args.bits}-g{args.group} dequant+GEMM, M={M} tokens x K={K} x N={N}, "
                                f"N split column-parallel over {world} rank(s) ({n_local} columns on rank 0)",
                    "M": M, "K": K, "N": N, "bits": args.bits, "group": args.group,
@@ -343,6 +347,18 @@ def main():
                            "ms_per_step": round(tr / args.steps * 1e3, 5),
                            "note": f"token-parallel replicas: each rank its own {M} tokens x the full weight"}
         full.close()
+    if world == 1:
+        # the rounded-weight mode on the same weights (side figure; same HIP-event timing)
+        lin16 = d.QuantLinear.from_weight(W, None, args.bits, args.group, d.linear.F16W)
+        for _ in range(args.warmup):
+            lin16(X, out=Y)
+        _, k16 = _timed(lambda: lin16(X, out=Y), args.steps, stream, torch, dist, world, dev)
+        t16 = flops_local / (k16 * 1e-3) / 1e12
+        out["f16_weights"] = {"kernel_ms": round(k16, 5), "achieved_tflops": round(t16, 1),
+                              "frac": round(t16 / PEAK_F16_TFLOPS, 4), "value": round(M / (k16 * 1e-3), 1),
+                              "note": "DLLM_PRECISION_F16W: weight rounded to f16 before the MFMA (~2.7e-4 "
+                                      "more relative error per layer); kernel time only"}
+        lin16.close()
     del W
     if not args.no_denoise:
         out["denoise_loop"] = denoise_loop(d, torch, dev)

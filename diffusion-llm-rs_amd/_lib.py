@@ -106,7 +106,10 @@ SIGNATURES = {
     "dllm_linear_export": (INT, [P, P, P, P, P]),
     "dllm_linear_info": (INT, [P, P, P, P, P]),
     "dllm_linear_weight_bytes": (S, [P]),
-    "dllm_linear_set_kernel_variant": (INT, [P, INT]),
+    "dllm_linear_device_bytes": (S, [P]),
+    "dllm_linear_create_ex": (INT, [P, P, S, S, U8, S, INT, P, P]),
+    "dllm_linear_create_quantized_ex": (INT, [P, P, P, P, S, S, U8, S, INT, P, P]),
+    "dllm_linear_precision": (INT, [P]),
     "dllm_linear_destroy": (INT, [P]),
     "dllm_kv_attention": (INT, [P, P, P, P, P, U8, S, S, S, P, P]),
     "dllm_beta_schedule": (INT, [INT, S, FL, FL, P]),
@@ -128,14 +131,24 @@ SIGNATURES = {
     "dllm_linear_forward_host": (INT, [P, P, S, P]),
 }
 
+# Exported only by the lab build (lib/libdllm_hip_lab.so, `make -C diffusion-llm-rs_amd/csrc lab`):
+# schedule variants and ablation masks for A/B measurement scripts.
+LAB_SIGNATURES = {
+    "dllm_linear_set_kernel_variant": (INT, [P, INT]),
+}
+LAB_LIB_PATH = PKG_DIR / "lib" / "libdllm_hip_lab.so"
+
 _lib = None
 
 
 def load(path: str | os.PathLike | None = None):
-    """Loads libdllm_hip.so (raises if absent: there is no CPU fallback)."""
+    """Loads libdllm_hip.so (raises if absent: there is no CPU fallback).  DLLM_LIB=lab selects the
+    lab build (measurement scripts only)."""
     global _lib
     if _lib is not None and path is None:
         return _lib
+    if path is None and os.environ.get("DLLM_LIB") == "lab":
+        path = LAB_LIB_PATH
     p = Path(path) if path else LIB_PATH
     if not p.exists():
         raise ImportError(f"{p} not built; run `python -c 'import __graft_entry__ as g; g.build()'` "
@@ -144,7 +157,11 @@ def load(path: str | os.PathLike | None = None):
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype, fn.argtypes = res, args
-    if path is None:
+    for name, (res, args) in LAB_SIGNATURES.items():
+        if hasattr(lib, name):
+            fn = getattr(lib, name)
+            fn.restype, fn.argtypes = res, args
+    if path is None or os.environ.get("DLLM_LIB") == "lab":
         _lib = lib
     return lib
 

@@ -120,6 +120,79 @@ __device__ __forceinline__ void store_out4(YT *yrow, const float *__restrict__ b
 
 constexpr int kMReps = kBM / 32;   // 8
 
+// Exact weight codes as f16: a b-bit field at bit position o of a 16-bit half (o + b <= 10) ORed into
+// the f16 2^(10-o) (ulp 2^-o) reads mag + q exactly, mag = 2^(10-o): one v_and_or_b32 per pair,
+// no shift.  Fields at o >= 8 cross the exponent and are read from the word shifted right by 8.
+// Then one exact v_pk_add_f16 of -(mag + zp) gives q - zp.
+struct ExactConsts {
+    uint32_t magic[5];   // f16 pairs 1024, 256, 64, 16, 4  (index = o / 2)
+    half2_t nz[5];       // -(mag + zp) pairs
+};
+
+__device__ __forceinline__ ExactConsts exact_consts(half2_t nz1024) {
+    ExactConsts c;
+    const uint32_t mags[5] = {0x64006400u, 0x5C005C00u, 0x54005400u, 0x4C004C00u, 0x44004400u};
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        uint32_t m = mags[i];
+        asm volatile("" : "+v"(m));   // a register operand: v_and_or_b32 takes no literal on gfx950
+        c.magic[i] = m;
+        const _Float16 d = static_cast<_Float16>(1024 - (1024 >> (2 * i)));   // 1024 - mag, exact
+        c.nz[i] = nz1024 + half2_t{d, d};                                     // -(mag + zp), exact
+    }
+    return c;
+}
+
+// The A fragment (8 f16) of substep s as exact integers (q - zp).
+template <int BITS>
+__device__ __forceinline__ half8_t dequant_exact(const uint32_t (&w)[BITS], int s, const ExactConsts &c) {
+    constexpr int PPW = 16 / BITS;
+    constexpr uint32_t mask = ((1u << BITS) - 1u) * 0x00010001u;
+    half8_t r;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        const int P = s * 4 + v;
+        const uint32_t word = w[P / PPW];
+        const int pos = BITS * (P % PPW);
+        const int o = pos + BITS <= 10 ? pos : pos - 8;
+        const uint32_t src = pos + BITS <= 10 ? word : (word >> 8);
+        const uint32_t t = (src & (mask << o)) | c.magic[o / 2];
+        const half2_t h = __builtin_bit_cast(half2_t, t) + c.nz[o / 2];
+        r[2 * v] = h[0];
+        r[2 * v + 1] = h[1];
+    }
+    return r;
+}
+
+
+// Split-K combine: Y[m][n] = sum_s ws[s][m][n] (slice order) + bias[n]; 4 outputs per thread.
+template <typename YT, int EPI = 0>
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const float *__restrict__ ws, int nsplit, int M, int N,
+                                                            int Npad, const float *__restrict__ bias,
+                                                            YT *__restrict__ Y, PSampleEpi epi = PSampleEpi{}) {
+    const int q = Npad / 4;
+    const size_t total = static_cast<size_t>(M) * q, slab = static_cast<size_t>(M) * Npad;
+    const bool vec_ok = (N % 4) == 0;
+    for (size_t i = blockIdx.x * static_cast<size_t>(256) + threadIdx.x; i < total;
+         i += static_cast<size_t>(gridDim.x) * 256) {
+        const int m = static_cast<int>(i / q), n = static_cast<int>(i % q) * 4;
+        if (n >= N) continue;
+        const float *p = ws + static_cast<size_t>(m) * Npad + n;
+        float4 a = *reinterpret_cast<const float4 *>(p);
+        for (int s = 1; s < nsplit; ++s) {
+            const float4 b = *reinterpret_cast<const float4 *>(p + s * slab);
+            a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+        }
+        if constexpr (EPI == 1) {
+            const float4 bv = *reinterpret_cast<const float4 *>(bias + n);
+            psample4(epi, m, n, N, a.x + bv.x, a.y + bv.y, a.z + bv.z, a.w + bv.w);
+        } else {
+            store_out4<YT>(Y + static_cast<size_t>(m) * N, bias, n, N, vec_ok, a.x, a.y, a.z, a.w);
+        }
+    }
+}
+
+
 
 template <int BITS>
 __device__ __forceinline__ void lds_words(uint32_t (&w)[BITS], const uint8_t *wbase, int lane) {
@@ -156,6 +229,23 @@ struct StageLayout8 {
 
 
 }  // namespace
+
+// Exact-weight GEMM (linear_exact.hip): Y = X . W^ + b with the MFMA A operand the exact integer
+// (q - zp) and the f32 scale folded once per group; wdev = prefill layout, sz = per (group, column)
+// f16 pair {-(1024+zp), *}, sf = f32 scales [G][Npad].  epi != null: fused p_sample into epi->x_prev.
+struct ExactGemmArgs {
+    int bits;
+    const __half *X;
+    int M, K;
+    const uint32_t *wdev, *sz;
+    const float *sf, *bias;
+    void *Y;
+    int N, Npad, group;
+    const PSampleEpi *epi;
+    int tm = 0;   // A/B: 256 x 256 tile-major tiles where they fill the chip
+};
+int launch_exact_gemm(const ExactGemmArgs &a, int y_f32, hipStream_t st);
+bool exact_gemm_supported(int M, int K, int Npad, int group);
 
 // Ping-pong 256 x 256 GEMM (linear_pp.hip): Y = X . W^ + b for the 256-column-tile grid, bits in
 // {2, 4, 8}, Y f16 (y_f32 = 0) or f32, epi != null: fused p_sample epilogue into epi->x_prev.

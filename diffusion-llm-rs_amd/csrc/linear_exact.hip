@@ -1,0 +1,439 @@
+// linear_exact.hip -- the group-quantized GEMM with EXACT dequantized weights (the default
+// prefill path of dllm_linear_forward for M > kDecodeMaxM).
+//
+// The reference layer is Y = X . W^ + b with W^[k][n] = (q - zp) * s[g][n] computed in f32
+// (diffuse-llm-rs/src/quantization.rs:81-85 per (column, 128-row group), lib.rs:806-813).  The
+// rounded path (wq_gemm8_kernel) feeds the MFMA f16((q - zp) * f16(s)): two f16 roundings of
+// every weight, ~2.7e-4 relative error per layer on top of X's own f16 rounding, and 1.17e-3
+// after config C5's 12-layer chain.  Here the MFMA A operand is (q - zp) itself -- an integer
+// below 2^11, so exact in f16 -- and the per-(group, column) scale is applied in f32 once per
+// group:  acc[m][n] += s[g][n] * T_g[m][n],  T_g = sum_{k in g} X[m][k] (q - zp)[k][n]  (MFMA,
+// f32 accumulation).  The only rounding left on the operands is X's (f16), ~2.1e-4 per layer.
+//
+// Tiles: block (32 MR tokens) x (32 NW columns), NW waves side by side in n; wave w owns columns
+// n0 + 32 w .. +32 for all 32 MR tokens, accumulators acc[MR] (running sum) and tacc[MR] (the
+// current group's T).  Yt = W^t Xt orientation as in linear_wq.hip: the accumulator lane is the
+// token, 4 consecutive registers are 4 consecutive columns (16-B f32 / 8-B f16 stores), and a
+// lane's 16 registers cover 16 columns whose scales it reads from LDS as 4 float4 per group.
+// Global -> LDS is LDS-DMA only (X tile XOR-swizzled, weight slab words, the group's zero-point
+// pair and f32 scale words) through a 3-stage ring with counted vmcnt waits and raw s_barrier,
+// as wq_gemm8_kernel.  Weight layout: the prefill ("fragment-major") layout of linear_wq.hip.
+#include "linear_common.hpp"
+
+#ifndef DLLM_LAB
+#define DLLM_LAB 0
+#endif
+
+#include <algorithm>
+#include <type_traits>
+#include <utility>
+
+namespace dllm {
+namespace {
+
+// A stage holds SPS consecutive 64-deep slabs (X tile, weight words) plus the group's zero-point
+// pairs and f32 scales; SPS = 2 makes a stage one 128-row group (one fold and one barrier per group).
+template <int BITS, int NW, int MR, int SPS>
+struct ExactStage {
+    static constexpr int kR1 = 4 * MR / NW;                // 1-KiB X pieces per wave per slab
+    static constexpr int kXRounds = SPS * kR1;
+    static constexpr int kX1 = 32 * MR * kBK * 2;           // one slab's X tile [32 MR][64] f16
+    static constexpr int kX = SPS * kX1;
+    static constexpr int kW1 = NW * 64 * BITS * 4;          // one slab's weight words
+    static constexpr int kW = SPS * kW1;
+    static constexpr int kSZ = 1024;                        // u32 {-(1024+zp)} pairs, 32 NW columns (+ mirror)
+    static constexpr int kSF = 1024;                        // f32 scales, 32 NW columns (+ mirror)
+    static constexpr int kBytes = kX + kW + kSZ + kSF;
+    static constexpr int kWOps = SPS * (BITS == 4 ? 1 : 2);
+    static_assert(kR1 >= 1 && 4 * MR % NW == 0, "X staging must split evenly over the waves");
+};
+
+// KPG: stages per group (group = 64 SPS KPG).  Slices of a split K are group-aligned.
+// TM (tile-major, 256 x 256 tiles, MR = 8, SPS = 1): each stage runs the token reps one after the
+// other -- 4 MFMAs of a rep into a transient accumulator (double-buffered by rep parity), then
+// that rep's fold with the group's scales -- so only 2 transient accumulators are live (a 128 + 256
+// register budget does not fit at two waves per SIMD).  Folding per 64-deep slab instead of per
+// group is the same sum: both slabs of a group carry the same scale.
+template <int BITS, typename YT, int NW, int MR, int SPS, int KPG, bool SPLIT = false, int EPI = 0, bool TM = false,
+          int TMB = 1>
+__global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2)
+wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdev,
+                     const uint32_t *__restrict__ sz, const float *__restrict__ sf, const float *__restrict__ bias,
+                     YT *__restrict__ Y, int N, int Npad, int group, int nbm, int nbn, int nsplit = 1,
+                     float *__restrict__ ws = nullptr, PSampleEpi epi = PSampleEpi{}) {
+    using SL = ExactStage<BITS, NW, MR, SPS>;
+    constexpr int kBMt = 32 * MR, kBNt = 32 * NW;
+    __shared__ __attribute__((aligned(16))) uint8_t st0[SL::kBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t st1[SL::kBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t st2[SL::kBytes];
+
+    // XCD-aware order: consecutive work items land on one XCD (blocks b, b+8 share an XCD under
+    // round-robin dispatch); K-slice outermost so an XCD's blocks share the slice's X rows in L2.
+    const int nb = nbm * nbn * nsplit, orig = blockIdx.x;
+    const int xcd = orig % kXCDs, q8 = nb / kXCDs, r8 = nb % kXCDs;
+    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / kXCDs;
+    const int ks = wgid / (nbm * nbn), tile = wgid % (nbm * nbn);
+    const int bm = tile / nbn, bn = tile % nbn;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int m0 = bm * kBMt, n0 = bn * kBNt;
+    const unsigned nk_all = static_cast<unsigned>(K) / kBK;                 // 64-deep slabs
+    const unsigned nk = nk_all / SPS / static_cast<unsigned>(nsplit);       // stages of this slice
+    const unsigned kt0 = static_cast<unsigned>(ks) * nk;
+    const unsigned spg = static_cast<unsigned>(group) / kBK;                // slabs per group
+    const unsigned nt = static_cast<unsigned>(n0 + wave * 32) >> 5;
+
+    const int chunk_st = lane & 7;
+    const __half *xsrc[SL::kR1];
+#pragma unroll
+    for (int i = 0; i < SL::kR1; ++i) {
+        const int row = (i * NW + wave) * 8 + (lane >> 3);
+        int grow = m0 + row;
+        grow = grow < M ? grow : M - 1;
+        const int c = chunk_st ^ ((row >> 1) & 7);
+        xsrc[i] = X + static_cast<size_t>(grow) * K + c * 8;
+    }
+    const uint32_t *wsrc = wdev + (static_cast<size_t>(nt) * nk_all * 64 + lane) * BITS;
+    const int ncol = lane & (8 * NW - 1);                    // 4 columns per lane (NW = 4: lanes 32.. mirror)
+    const uint32_t *szsrc = sz + n0 + 4 * ncol;
+    const float *sfsrc = sf + n0 + 4 * ncol;
+    const bool has_sz = wave == 0, has_sf = wave == 1;
+    const uint32_t wv = static_cast<uint32_t>(wave);
+
+    // LDS destinations go through readfirstlane: the M0 operand must be an SGPR, and hipcc's
+    // divergence analysis does not prove it uniform through the unrolled ring.
+    auto u = [](uint32_t v) { return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(v))); };
+    auto stage = [&](uint8_t *sb, unsigned kt) __attribute__((always_inline)) {
+        const uint32_t base = u(lds_addr(sb));
+        const unsigned slab0 = (kt + kt0) * SPS;
+#pragma unroll
+        for (int s = 0; s < SPS; ++s)
+#pragma unroll
+            for (int i = 0; i < SL::kR1; ++i)
+                glds16_asm(xsrc[i] + (slab0 + s) * kBK, u(base + s * SL::kX1 + wv * 1024 + i * NW * 1024));
+#pragma unroll
+        for (int s = 0; s < SPS; ++s) {
+            const uint32_t *wp = wsrc + static_cast<size_t>(slab0 + s) * 64 * BITS;
+            const uint32_t wb = u(base + SL::kX + s * SL::kW1 + wv * (64 * BITS * 4));
+            if constexpr (BITS == 4) {
+                glds16_asm(wp, wb);
+            } else if constexpr (BITS == 8) {
+                glds16_asm(wp, wb);
+                glds16_asm(wp + 4, u(wb + 64 * 16));
+            } else {
+                glds4_asm(wp, wb);
+                glds4_asm(wp + 1, u(wb + 256));
+            }
+        }
+        const size_t goff = static_cast<size_t>(slab0 / spg) * Npad;
+        if (has_sz) glds16_asm(szsrc + goff, u(base + SL::kX + SL::kW));
+        if (has_sf) glds16_asm(sfsrc + goff, u(base + SL::kX + SL::kW + SL::kSZ));
+    };
+    // Counted wait leaving the newest stage's DMAs (this wave's own count) in flight.
+    auto wait_prev = [&]() __attribute__((always_inline)) {
+        if (has_sz || has_sf) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kXRounds + SL::kWOps + 1) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kXRounds + SL::kWOps) : "memory");
+    };
+
+    float16_t acc[MR], tacc[TM ? TMB : MR];
+#pragma unroll
+    for (int r = 0; r < MR; ++r)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[r][e] = 0.0f;
+    const float16_t zero16 = {};
+
+    const int hsel = lane >> 5;
+    const int rowx = ((lane & 31) >> 1) & 7;
+    int soff[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) soff[j] = (lane & 31) * (kBK * 2) + ((((2 * j + hsel) ^ rowx)) << 4);
+
+    // B fragments of substep v (slab v / 4, 16-deep step v % 4) for the MR token reps.
+    auto read_b = [&](half8_t (&b)[MR], const uint8_t *sb, int v) __attribute__((always_inline)) {
+#pragma unroll
+        for (int r = 0; r < MR; ++r)
+            b[r] = *reinterpret_cast<const half8_t *>(sb + (v / 4) * SL::kX1 + soff[v % 4] + r * 32 * kBK * 2);
+    };
+
+    // One stage (SPS slabs) on sb; stage pf receives stage kt + 2.  GF: first stage of a group (the
+    // group's first MFMA starts from zero); GL: last (fold the group into acc with its scales).
+    auto step = [&](const uint8_t *sb, uint8_t *pf, unsigned kt, auto gf_tag, auto gl_tag) __attribute__((always_inline)) {
+        constexpr bool GF = decltype(gf_tag)::value, GL = decltype(gl_tag)::value;
+        constexpr int kSub = 4 * SPS;
+        const bool issue = kt + 2 < nk;
+        if (issue) stage(pf, kt + 2);
+        uint32_t w[SPS][BITS];
+#pragma unroll
+        for (int s = 0; s < SPS; ++s) lds_words<BITS>(w[s], sb + SL::kX + s * SL::kW1 + wave * (64 * BITS * 4), lane);
+        const half2_t p = __builtin_bit_cast(half2_t,
+                                             *reinterpret_cast<const uint32_t *>(sb + SL::kX + SL::kW + (wave * 32 + (lane & 31)) * 4));
+        const ExactConsts ec = exact_consts(half2_t{p[0], p[0]});
+        half8_t bA[MR], bB[MR];
+        read_b(bA, sb, 0);
+        half8_t aA = dequant_exact<BITS>(w[0], 0, ec), aB;
+        auto sub = [&](half8_t (&bc)[MR], half8_t (&bn)[MR], const half8_t &ac, half8_t &an, auto v_tag) __attribute__((always_inline)) {
+            constexpr int v = decltype(v_tag)::value;
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_setprio(1);
+            if constexpr (v + 1 < kSub) {
+                read_b(bn, sb, v + 1);
+                an = dequant_exact<BITS>(w[(v + 1) / 4], (v + 1) % 4, ec);
+            }
+#pragma unroll
+            for (int r = 0; r < MR; ++r)
+                tacc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bc[r], (GF && v == 0) ? zero16 : tacc[r], 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < MR; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);   // VALU
+            }
+            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        [&]<int... Vs>(std::integer_sequence<int, Vs...>) __attribute__((always_inline)) {
+            ((Vs % 2 == 0 ? sub(bA, bB, aA, aB, std::integral_constant<int, Vs>{})
+                          : sub(bB, bA, aB, aA, std::integral_constant<int, Vs>{})), ...);
+        }(std::make_integer_sequence<int, kSub>{});
+        if constexpr (GL) {
+            // acc += s (.) T_g: lane half hsel holds columns 4 hsel + 8 qd + (0..3) of the wave's 32.
+            const float *sfl = reinterpret_cast<const float *>(sb + SL::kX + SL::kW + SL::kSZ) + wave * 32 + 4 * hsel;
+            float4 s4[4];
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd) s4[qd] = *reinterpret_cast<const float4 *>(sfl + 8 * qd);
+#pragma unroll
+            for (int r = 0; r < MR; ++r)
+#pragma unroll
+                for (int qd = 0; qd < 4; ++qd) {
+                    acc[r][4 * qd + 0] = __builtin_fmaf(s4[qd].x, tacc[r][4 * qd + 0], acc[r][4 * qd + 0]);
+                    acc[r][4 * qd + 1] = __builtin_fmaf(s4[qd].y, tacc[r][4 * qd + 1], acc[r][4 * qd + 1]);
+                    acc[r][4 * qd + 2] = __builtin_fmaf(s4[qd].z, tacc[r][4 * qd + 2], acc[r][4 * qd + 2]);
+                    acc[r][4 * qd + 3] = __builtin_fmaf(s4[qd].w, tacc[r][4 * qd + 3], acc[r][4 * qd + 3]);
+                }
+        }
+        // Stage kt+1 must have landed; kt+2's DMAs may stay in flight across the barrier.
+        if (issue) wait_prev();
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto step_tm = [&](const uint8_t *sb, uint8_t *pf, unsigned kt) __attribute__((always_inline)) {
+        const bool issue = kt + 2 < nk;
+        if (issue) stage(pf, kt + 2);
+        uint32_t w[BITS];
+        lds_words<BITS>(w, sb + SL::kX + wave * (64 * BITS * 4), lane);
+        const half2_t p = __builtin_bit_cast(half2_t,
+                                             *reinterpret_cast<const uint32_t *>(sb + SL::kX + SL::kW + (wave * 32 + (lane & 31)) * 4));
+        const ExactConsts ec = exact_consts(half2_t{p[0], p[0]});
+        const float *sfl = reinterpret_cast<const float *>(sb + SL::kX + SL::kW + SL::kSZ) + wave * 32 + 4 * hsel;
+        float4 s4[4];
+#pragma unroll
+        for (int qd = 0; qd < 4; ++qd) s4[qd] = *reinterpret_cast<const float4 *>(sfl + 8 * qd);
+        half8_t a[4], bq[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[j] = dequant_exact<BITS>(w, j, ec);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bq[j] = *reinterpret_cast<const half8_t *>(sb + soff[j]);
+        auto fold = [&](int r) __attribute__((always_inline)) {
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd) {
+                acc[r][4 * qd + 0] = __builtin_fmaf(s4[qd].x, tacc[r % TMB][4 * qd + 0], acc[r][4 * qd + 0]);
+                acc[r][4 * qd + 1] = __builtin_fmaf(s4[qd].y, tacc[r % TMB][4 * qd + 1], acc[r][4 * qd + 1]);
+                acc[r][4 * qd + 2] = __builtin_fmaf(s4[qd].z, tacc[r % TMB][4 * qd + 2], acc[r][4 * qd + 2]);
+                acc[r][4 * qd + 3] = __builtin_fmaf(s4[qd].w, tacc[r % TMB][4 * qd + 3], acc[r][4 * qd + 3]);
+            }
+        };
+#pragma unroll
+        for (int r = 0; r < MR; ++r) {
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_setprio(1);
+            // MFMA j of rep r reads bq[j]; the next rep's fragment j refills it right after.
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                tacc[r % TMB] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[j], bq[j], j == 0 ? zero16 : tacc[r % TMB], 0, 0, 0);
+                if (r + 1 < MR) bq[j] = *reinterpret_cast<const half8_t *>(sb + soff[j] + (r + 1) * 32 * kBK * 2);
+            }
+            if constexpr (TMB == 1) {
+                fold(r);
+                // Pin the order: the fold of rep r completes before rep r+1's MFMAs (their B
+                // fragments pass through this statement), so only one transient accumulator lives.
+                asm volatile("" : "+v"(acc[r]), "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]));
+            } else if (r > 0) {
+                fold(r - 1);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+                __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);   // VALU (the previous rep's fold)
+            }
+            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (TMB > 1) fold(MR - 1);
+        if (issue) wait_prev();
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // The ring rotates with period 3 and the group phase with period KPG: unroll lcm(3, KPG)
+    // stages so every stage's buffer and group phase are compile-time (a run-time phase
+    // dispatch made hipcc spill ~80 VGPRs).
+    auto at = [&](auto i_tag, unsigned kt) __attribute__((always_inline)) {
+        constexpr int I = decltype(i_tag)::value;
+        constexpr int cur = I % 3, nxt = (I + 2) % 3;
+        uint8_t *sb = cur == 0 ? st0 : (cur == 1 ? st1 : st2);
+        uint8_t *pf = nxt == 0 ? st0 : (nxt == 1 ? st1 : st2);
+        if constexpr (TM) step_tm(sb, pf, kt);
+        else step(sb, pf, kt, std::integral_constant<bool, I % KPG == 0>{},
+                  std::integral_constant<bool, I % KPG == KPG - 1>{});
+    };
+    constexpr int kUnroll = (KPG == 1 || TM) ? 3 : (KPG == 2 ? 6 : 12);
+
+    stage(st0, 0);
+    if (nk > 1) stage(st1, 1);
+    if (nk > 1) wait_prev();
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    for (unsigned kt = 0; kt < nk; kt += kUnroll) {
+        [&]<int... Is>(std::integer_sequence<int, Is...>) __attribute__((always_inline)) {
+            ((kt + Is < nk ? (at(std::integral_constant<int, Is>{}, kt + Is), 0) : 0), ...);
+        }(std::make_integer_sequence<int, kUnroll>{});
+    }
+
+    // Epilogue: acc[r] reg e -> n = n0 + 32 wave + 4 hsel + 8 (e >> 2) + (e & 3), m = m0 + 32 r + (lane & 31).
+    const int nb0 = n0 + wave * 32 + 4 * hsel;
+    if constexpr (SPLIT) {
+        float *slab = ws + static_cast<size_t>(ks) * M * Npad;
+#pragma unroll
+        for (int r = 0; r < MR; ++r) {
+            const int m = m0 + r * 32 + (lane & 31);
+            if (m >= M) continue;
+            float *prow = slab + static_cast<size_t>(m) * Npad + nb0;
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd)
+                *reinterpret_cast<float4 *>(prow + 8 * qd) =
+                    make_float4(acc[r][4 * qd + 0], acc[r][4 * qd + 1], acc[r][4 * qd + 2], acc[r][4 * qd + 3]);
+        }
+        return;
+    }
+    float4 bv[4];
+#pragma unroll
+    for (int qd = 0; qd < 4; ++qd) bv[qd] = *reinterpret_cast<const float4 *>(bias + nb0 + 8 * qd);
+    if constexpr (EPI == 1) {
+#pragma unroll
+        for (int r = 0; r < MR; ++r) {
+            const int m = m0 + r * 32 + (lane & 31);
+            if (m >= M) continue;
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd) {
+                if (nb0 + 8 * qd >= N) continue;
+                psample4(epi, m, nb0 + 8 * qd, N, acc[r][4 * qd + 0] + bv[qd].x, acc[r][4 * qd + 1] + bv[qd].y,
+                         acc[r][4 * qd + 2] + bv[qd].z, acc[r][4 * qd + 3] + bv[qd].w);
+            }
+        }
+        return;
+    }
+    const bool full = (m0 + kBMt <= M) && (n0 + kBNt <= N) && (N % 4) == 0;
+    if (full) {
+#pragma unroll
+        for (int r = 0; r < MR; ++r) {
+            YT *yrow = Y + static_cast<size_t>(m0 + r * 32 + (lane & 31)) * N + nb0;
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd)
+                store4<YT>(yrow + 8 * qd, acc[r][4 * qd + 0] + bv[qd].x, acc[r][4 * qd + 1] + bv[qd].y,
+                           acc[r][4 * qd + 2] + bv[qd].z, acc[r][4 * qd + 3] + bv[qd].w);
+        }
+    } else {
+        const bool vec_ok = (N % 4) == 0;
+#pragma unroll
+        for (int r = 0; r < MR; ++r) {
+            const int m = m0 + r * 32 + (lane & 31);
+            if (m >= M) continue;
+            YT *yrow = Y + static_cast<size_t>(m) * N;
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd)
+                store_out4<YT>(yrow, bias, nb0 + 8 * qd, N, vec_ok, acc[r][4 * qd + 0], acc[r][4 * qd + 1],
+                               acc[r][4 * qd + 2], acc[r][4 * qd + 3]);
+        }
+    }
+}
+
+template <int BITS, typename YT, int NW, int MR, int SPS, int KPG, int EPI, bool TM = false>
+int launch_exact_tile(const ExactGemmArgs &a, int nsplit, hipStream_t st) {
+    const int nbm = (a.M + 32 * MR - 1) / (32 * MR), nbn = a.Npad / (32 * NW);
+    const unsigned nb = static_cast<unsigned>(nbm * nbn * nsplit);
+    const PSampleEpi ep = a.epi ? *a.epi : PSampleEpi{};
+    YT *Y = static_cast<YT *>(a.Y);
+    if (nsplit == 1) {
+        wq_gemm_exact_kernel<BITS, YT, NW, MR, SPS, KPG, false, EPI, TM><<<nb, NW * 64, 0, st>>>(
+            a.X, a.M, a.K, a.wdev, a.sz, a.sf, a.bias, Y, a.N, a.Npad, a.group, nbm, nbn, 1, nullptr, ep);
+        DLLM_LAUNCH_CHECK();
+        return DLLM_OK;
+    }
+    float *ws = device_workspace(st, static_cast<size_t>(nsplit) * a.M * a.Npad * sizeof(float));
+    if (!ws) return DLLM_ERR_HIP;
+    wq_gemm_exact_kernel<BITS, YT, NW, MR, SPS, KPG, true, 0, TM><<<nb, NW * 64, 0, st>>>(
+        a.X, a.M, a.K, a.wdev, a.sz, a.sf, a.bias, Y, a.N, a.Npad, a.group, nbm, nbn, nsplit, ws);
+    DLLM_LAUNCH_CHECK();
+    const size_t q = static_cast<size_t>(a.M) * (a.Npad / 4);
+    const unsigned rb = static_cast<unsigned>(std::min<size_t>((q + 255) / 256, 4 * kCUs));
+    splitk_reduce_kernel<YT, EPI><<<rb, 256, 0, st>>>(ws, nsplit, a.M, a.N, a.Npad, a.bias, Y, ep);
+    DLLM_LAUNCH_CHECK();
+    return DLLM_OK;
+}
+
+// Tile policy: 128 x 256 tiles (8 waves, two per SIMD; stages of one 128-row group) when they give
+// >= 256 blocks; otherwise 128 x 128 tiles (4 waves, two blocks per CU, 64-deep stages) with K
+// split over group-aligned slices until the grid has >= ~200 blocks.  G64 = group / 64.
+template <int BITS, typename YT, int G64, int EPI>
+int launch_exact_bits(const ExactGemmArgs &a, hipStream_t st) {
+    const int mb = (a.M + 127) / 128;
+#if DLLM_LAB
+    if (a.tm && a.Npad % 256 == 0 && ((a.M + 255) / 256) * (a.Npad / 256) >= kCUs)
+        return launch_exact_tile<BITS, YT, 8, 8, 1, G64, EPI, true>(a, 1, st);
+#endif
+    if (a.Npad % 256 == 0 && mb * (a.Npad / 256) >= kCUs) {
+        // int8 weights: one-slab stages (two-slab stages exceed the 160 KiB LDS ring)
+        if constexpr (G64 == 1 || BITS == 8) return launch_exact_tile<BITS, YT, 8, 4, 1, G64, EPI>(a, 1, st);
+        else return launch_exact_tile<BITS, YT, 8, 4, 2, G64 / 2, EPI>(a, 1, st);
+    }
+    const int tiles = mb * (a.Npad / 128), ngroups = a.K / a.group;
+    int nsplit = 1;
+    while (tiles * nsplit < 200 && nsplit < 8 && ngroups % (2 * nsplit) == 0 && (a.K / kBK) / (2 * nsplit) >= 4)
+        nsplit *= 2;
+    return launch_exact_tile<BITS, YT, 4, 4, 1, G64, EPI>(a, nsplit, st);
+}
+
+template <int KPG, int EPI>
+int launch_exact_kpg(const ExactGemmArgs &a, int y_f32, hipStream_t st) {
+    switch (a.bits) {
+    case 2: return EPI || y_f32 ? launch_exact_bits<2, float, KPG, EPI>(a, st) : launch_exact_bits<2, __half, KPG, 0>(a, st);
+    case 4: return EPI || y_f32 ? launch_exact_bits<4, float, KPG, EPI>(a, st) : launch_exact_bits<4, __half, KPG, 0>(a, st);
+    case 8: return EPI || y_f32 ? launch_exact_bits<8, float, KPG, EPI>(a, st) : launch_exact_bits<8, __half, KPG, 0>(a, st);
+    default: return fail(DLLM_ERR_UNSUPPORTED, "bits");
+    }
+}
+
+}  // namespace
+
+bool exact_gemm_supported(int M, int K, int Npad, int group) {
+    return M >= 1 && Npad % 128 == 0 && K % group == 0 && (group == 64 || group == 128 || group == 256);
+}
+
+int launch_exact_gemm(const ExactGemmArgs &a, int y_f32, hipStream_t st) {
+    if (!exact_gemm_supported(a.M, a.K, a.Npad, a.group))
+        return fail(DLLM_ERR_SHAPE_MISMATCH, "exact GEMM: needs Npad % 128 == 0, group in {64, 128, 256}, K % group == 0");
+    const bool fused = a.epi != nullptr;
+    switch (a.group / kBK) {
+    case 1: return fused ? launch_exact_kpg<1, 1>(a, 1, st) : launch_exact_kpg<1, 0>(a, y_f32, st);
+    case 2: return fused ? launch_exact_kpg<2, 1>(a, 1, st) : launch_exact_kpg<2, 0>(a, y_f32, st);
+    default: return fused ? launch_exact_kpg<4, 1>(a, 1, st) : launch_exact_kpg<4, 0>(a, y_f32, st);
+    }
+}
+
+}  // namespace dllm

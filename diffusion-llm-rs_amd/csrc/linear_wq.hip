@@ -19,6 +19,10 @@
 #include "linear_common.hpp"
 #include "diffusion_rng.hpp"
 
+#ifndef DLLM_LAB
+#define DLLM_LAB 0
+#endif
+
 #include <algorithm>
 #include <map>
 #include <tuple>
@@ -32,22 +36,25 @@ struct dllm_linear {
     size_t K = 0, N = 0, Npad = 0, G = 0, group = 0;
     int bits = 0;
     int device = 0;
+    int precision = DLLM_PRECISION_EXACT;
     uint32_t *wdev = nullptr;     // prefill layout (32x32x16 fragments)
     uint32_t *wdec = nullptr;     // decode layout (16x16x32 fragments)
-    uint32_t *w16 = nullptr;      // 16x16x32 prefill layout (wq_gemm16_kernel)
-    uint32_t *sz = nullptr;       // [G][Npad]
-    uint32_t *canon = nullptr;    // canonical packed codes (u32-padded)
+    uint32_t *sz = nullptr;       // [G][Npad] f16 pairs {-(1024 + zp), f16(scale)}
+    float *sf = nullptr;          // [G][Npad] f32 scales (exact-weight kernels), 0 in the padding
     float *scales = nullptr;      // [G][N]
     uint8_t *zps = nullptr;       // [G][N]
     float *bias = nullptr;        // [Npad]
     __half *xws = nullptr;        // f32 -> f16 staging for X
     size_t xws_elems = 0;
-    int variant = 4;              // prefill schedule variant (tuning knob, see wq_gemm_kernel)
-    int dlab = 0;                 // decode-kernel ablation mask (measurement only; 0 in production)
-    int dcfg = 0;                 // decode (NT, nsplit) override (measurement knob; 0 = policy)
-    int rlab = 0;                 // ring-kernel ablation mask (measurement only; 0 in production)
-    int pplab = 0;                // ping-pong-kernel ablation mask (measurement only; 0 in production)
     std::mutex mu;
+#if DLLM_LAB   // measurement knobs of the lab build (dllm_linear_set_kernel_variant)
+    uint32_t *w16 = nullptr;      // 16x16x32 prefill layout (wq_gemm16_kernel)
+    int variant = -1;             // prefill schedule variant (-1: product policy)
+    int dlab = 0;                 // decode-kernel ablation mask
+    int dcfg = 0;                 // decode (NT, nsplit) override
+    int rlab = 0;                 // ring-kernel ablation mask
+    int pplab = 0;                // ping-pong-kernel ablation mask
+#endif
 };
 
 namespace dllm {
@@ -194,6 +201,7 @@ __global__ void __launch_bounds__(256) build_fragments_kernel(const uint32_t *__
     }
 }
 
+#if DLLM_LAB   // lab build only
 // Canonical -> 16x16x32 prefill layout: [32-column tile][k64 slab][lane][bits words], lane l,
 // "substep" S' = 2 f + s (f: 16-column half of the tile, s: 32-deep half of the slab), code j of
 // the lane's 8 = column 32 nt + 16 f + (l & 15), k = 64 slab + 32 s + 8 (l >> 4) + j; words and
@@ -224,6 +232,8 @@ __global__ void __launch_bounds__(256) build_fragments16_kernel(const uint32_t *
     }
 }
 
+#endif  // DLLM_LAB
+
 // Canonical -> decode layout.  One thread per (column n < Npad, 128-deep slab).
 __global__ void __launch_bounds__(256) build_decode_kernel(const uint32_t *__restrict__ canon, size_t K, size_t N,
                                                            size_t Npad, int bits, uint32_t *__restrict__ wdec) {
@@ -249,6 +259,31 @@ __global__ void __launch_bounds__(256) build_decode_kernel(const uint32_t *__res
     }
 }
 
+// Fragment-major (prefill layout) -> canonical packed bytes: one thread per output byte; code
+// (k, n) sits in wdev word ((n/32 * K/64 + k/64) * 64 + lane) * bits + P / (16/bits), lane =
+// (n & 31) + 32 ((k % 16) / 8), pair P = 4 ((k % 64) / 16) + (k % 8) / 2, at bit
+// bits (P % (16/bits)) + 16 (k & 1).  Inverse of build_fragments_kernel (export round trip test).
+__global__ void __launch_bounds__(256) export_codes_kernel(const uint32_t *__restrict__ wdev, size_t K, size_t N,
+                                                           int bits, uint8_t *__restrict__ out, size_t nbytes) {
+    const size_t nk = K / 64, ppw = 16 / bits, per_byte = 8 / bits;
+    const uint32_t mask = (1u << bits) - 1u;
+    for (size_t B = blockIdx.x * static_cast<size_t>(256) + threadIdx.x; B < nbytes;
+         B += static_cast<size_t>(gridDim.x) * 256) {
+        uint32_t byte = 0;
+        for (size_t e = 0; e < per_byte; ++e) {
+            const size_t i = B * per_byte + e;
+            if (i >= K * N) break;
+            const size_t k = i / N, n = i % N;
+            const size_t kk = k % 64, lane = (n & 31) + 32 * ((kk % 16) / 8);
+            const size_t P = 4 * (kk / 16) + (kk % 8) / 2;
+            const uint32_t word = wdev[(((n >> 5) * nk + k / 64) * 64 + lane) * bits + P / ppw];
+            const uint32_t code = (word >> (bits * (P % ppw) + 16 * (k & 1))) & mask;
+            byte |= code << (bits * e);
+        }
+        out[B] = static_cast<uint8_t>(byte);
+    }
+}
+
 __global__ void __launch_bounds__(256) build_sz_kernel(const float *__restrict__ scales, const uint8_t *__restrict__ zps,
                                                        size_t G, size_t N, size_t Npad, uint32_t *__restrict__ sz) {
     const size_t n = blockIdx.x * static_cast<size_t>(256) + threadIdx.x;
@@ -260,6 +295,13 @@ __global__ void __launch_bounds__(256) build_sz_kernel(const float *__restrict__
     pk.h[0] = static_cast<_Float16>(nz);   // exact (integer < 2048)
     pk.h[1] = static_cast<_Float16>(s);    // RNE
     sz[g * Npad + n] = pk.u;
+}
+
+__global__ void __launch_bounds__(256) build_sf_kernel(const float *__restrict__ scales, size_t G, size_t N,
+                                                       size_t Npad, float *__restrict__ sf) {
+    const size_t n = blockIdx.x * static_cast<size_t>(256) + threadIdx.x;
+    const size_t g = blockIdx.y;
+    if (n < Npad) sf[g * Npad + n] = n < N ? scales[g * N + n] : 0.0f;
 }
 
 __global__ void __launch_bounds__(256) cast_f32_f16_kernel(const float *__restrict__ x, size_t n,
@@ -288,19 +330,7 @@ __global__ void __launch_bounds__(256) expand_coef_kernel(const float *__restric
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Prefill GEMM (M > decode threshold): Y[M][N] = X[M][K] (f16) . W^[K][N] + b, computed as
-// Y^T = W^^T X^T so that the accumulator's lane index is the token m and 4 consecutive
-// registers hold 4 consecutive output columns n (one 8/16-byte store each).
-//   block tile 256 (m) x 128 (n), 4 waves side by side in n, wave tile 256 (m) x 32 (n):
-//   acc[8 m-reps] of 32x32 f32 = 128 VGPRs.  Each wave dequantizes only its own 32 columns
-//   (no redundant dequant; 2.5 VALU per MFMA) and all 4 waves share the X tile.
-//   X tile [256][64] f16 in LDS (2 stages, 64 KiB -> 2 blocks per CU), filled by
-//   global_load_lds 16 B/lane with the 16-B chunk index XOR-swizzled by (row>>1)&7
-//   (conflict-free ds_read_b128 fragments, measured SQ_LDS_BANK_CONFLICT = 0).
-//   W fragments stream straight to VGPRs, one coalesced dwordx4 per lane per 64-deep slab
-//   (int4), one slab ahead.
-// ---------------------------------------------------------------------------------------------
+// Loads a lane's BITS weight words (one 16-B or 8-B vector).
 template <int BITS>
 __device__ __forceinline__ void load_words(uint32_t (&w)[BITS], const uint32_t *__restrict__ p) {
     if constexpr (BITS == 4) {
@@ -316,6 +346,20 @@ __device__ __forceinline__ void load_words(uint32_t (&w)[BITS], const uint32_t *
     }
 }
 
+#if DLLM_LAB   // lab build only
+// ---------------------------------------------------------------------------------------------
+// Prefill GEMM (M > decode threshold): Y[M][N] = X[M][K] (f16) . W^[K][N] + b, computed as
+// Y^T = W^^T X^T so that the accumulator's lane index is the token m and 4 consecutive
+// registers hold 4 consecutive output columns n (one 8/16-byte store each).
+//   block tile 256 (m) x 128 (n), 4 waves side by side in n, wave tile 256 (m) x 32 (n):
+//   acc[8 m-reps] of 32x32 f32 = 128 VGPRs.  Each wave dequantizes only its own 32 columns
+//   (no redundant dequant; 2.5 VALU per MFMA) and all 4 waves share the X tile.
+//   X tile [256][64] f16 in LDS (2 stages, 64 KiB -> 2 blocks per CU), filled by
+//   global_load_lds 16 B/lane with the 16-B chunk index XOR-swizzled by (row>>1)&7
+//   (conflict-free ds_read_b128 fragments, measured SQ_LDS_BANK_CONFLICT = 0).
+//   W fragments stream straight to VGPRs, one coalesced dwordx4 per lane per 64-deep slab
+//   (int4), one slab ahead.
+// ---------------------------------------------------------------------------------------------
 // LDS stage layout (bytes): X tile [256][64] f16 (32 KiB) | W slabs [4 waves][64 lanes][BITS words]
 // | sz [4 waves][64 lanes] u32.  Everything arrives by global_load_lds, so hipcc's counters see no
 // register-destination global load in the loop (mixing the two kinds makes it wait vmcnt(0) at
@@ -527,6 +571,8 @@ wq_gemm_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__res
         }
     }
 }
+
+#endif  // DLLM_LAB
 
 // ---------------------------------------------------------------------------------------------
 // Big-tile prefill GEMM (used when it still fills the chip): block tile 256 (m) x 256 (n), 8 waves
@@ -831,6 +877,7 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
     }
 }
 
+#if DLLM_LAB   // lab build only
 // 256 x 256 ring GEMM with the 2 (m) x 4 (n) wave layout: wave (rm, cg) = (wave / 4, wave % 4) owns
 // rows m0 + 128 rm .. +128 (4 m-reps) and columns n0 + 64 cg .. +64 (two 32-column fragments), so
 // each B fragment read from LDS feeds two MFMAs (half the LDS read traffic of the 1 x 8 layout of
@@ -1212,32 +1259,7 @@ wq_gemm16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
     }
 }
 
-// Split-K combine: Y[m][n] = sum_s ws[s][m][n] (slice order) + bias[n]; 4 outputs per thread.
-template <typename YT, int EPI = 0>
-__global__ void __launch_bounds__(256) splitk_reduce_kernel(const float *__restrict__ ws, int nsplit, int M, int N,
-                                                            int Npad, const float *__restrict__ bias,
-                                                            YT *__restrict__ Y, PSampleEpi epi = PSampleEpi{}) {
-    const int q = Npad / 4;
-    const size_t total = static_cast<size_t>(M) * q, slab = static_cast<size_t>(M) * Npad;
-    const bool vec_ok = (N % 4) == 0;
-    for (size_t i = blockIdx.x * static_cast<size_t>(256) + threadIdx.x; i < total;
-         i += static_cast<size_t>(gridDim.x) * 256) {
-        const int m = static_cast<int>(i / q), n = static_cast<int>(i % q) * 4;
-        if (n >= N) continue;
-        const float *p = ws + static_cast<size_t>(m) * Npad + n;
-        float4 a = *reinterpret_cast<const float4 *>(p);
-        for (int s = 1; s < nsplit; ++s) {
-            const float4 b = *reinterpret_cast<const float4 *>(p + s * slab);
-            a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
-        }
-        if constexpr (EPI == 1) {
-            const float4 bv = *reinterpret_cast<const float4 *>(bias + n);
-            psample4(epi, m, n, N, a.x + bv.x, a.y + bv.y, a.z + bv.z, a.w + bv.w);
-        } else {
-            store_out4<YT>(Y + static_cast<size_t>(m) * N, bias, n, N, vec_ok, a.x, a.y, a.z, a.w);
-        }
-    }
-}
+#endif  // DLLM_LAB
 
 // ---------------------------------------------------------------------------------------------
 // Decode GEMM (small M, weight-streaming / HBM-bound): one block per 16 NT-column group and
@@ -1254,11 +1276,14 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float *__restr
 typedef float float4_t __attribute__((ext_vector_type(4)));
 constexpr int kDecWaves = 8;
 
-template <int BITS, typename YT, int MT, int NT = 1, bool SPLIT = false, int LAB = 0>
+// EXACT: the MFMA A operand is the exact integer (q - zp) (linear_exact.hip) and each slab's
+// partial is folded into the accumulator with the f32 scales of its group(s) (group 64: two folds
+// per 128-deep slab; group >= 128: one).
+template <int BITS, typename YT, int MT, int NT = 1, bool SPLIT = false, int LAB = 0, bool EXACT = false>
 __global__ void __launch_bounds__(kDecWaves * 64)
 wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdec,
                  const uint32_t *__restrict__ sz, const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad,
-                 int group, int nsplit = 1, float *__restrict__ ws = nullptr) {
+                 int group, int nsplit = 1, float *__restrict__ ws = nullptr, const float *__restrict__ sf = nullptr) {
     // Slabs in flight per wave: every load of a round (W words, scales, X fragments) is issued
     // before the first MFMA, so a round costs one memory latency, not one per 32-deep step.
     // The load phase has no branch and every loop bound is wave-uniform (scalar wave index): a
@@ -1267,7 +1292,7 @@ wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
     // slabs of the last round read X through a buffer resource with an out-of-range offset, which
     // returns zeros without a memory access; X is thereby also free of per-lane selects.
     // Rounds of slabs in flight per wave, sized to the registers one slab's operands take.
-    constexpr int kPerSlab = NT * BITS + NT + 16 * MT;
+    constexpr int kPerSlab = NT * BITS + NT + 16 * MT + (EXACT ? 8 * NT : 0);
     constexpr int kDepth = NT == 1 ? (MT <= 2 ? 4 : 2) : (128 / kPerSlab < 1 ? 1 : (128 / kPerSlab > 4 ? 4 : 128 / kPerSlab));
     constexpr uint32_t kOOB = 0x80000000u;
     __shared__ __attribute__((aligned(16))) float red[kDecWaves * MT * NT * 64 * 4];
@@ -1305,10 +1330,12 @@ wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = float4_t{0.f, 0.f, 0.f, 0.f};
 
+    const bool g64 = group == 64;   // EXACT: two groups per 128-deep slab
     for (int base = s_beg + wave; base < s_end; base += kDecWaves * kDepth) {
         uint32_t w[kDepth][NT][BITS];
         uint32_t szl[kDepth][NT];
         half8_t xb[kDepth][4][MT];
+        float4 sfl[kDepth][NT][EXACT ? 2 : 1];
 #pragma unroll
         for (int i = 0; i < kDepth; ++i) {
             const int slab_raw = base + i * kDecWaves;
@@ -1324,6 +1351,13 @@ wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
                 }
                 if constexpr (LAB & 2) szl[i][nt] = 0x3c00e400u + ks;
                 else szl[i][nt] = szcol[static_cast<size_t>(ks / group) * Npad + 16 * nt];
+                if constexpr (EXACT) {
+                    // scales of this lane's 4 columns for the slab's group (group 64: both halves)
+                    const int nb0 = n0 + 16 * nt + 4 * (lane >> 4);
+                    const int g0 = (slab * 128) / group, g1 = g64 ? min(g0 + 1, (K - 1) / group) : g0;
+                    sfl[i][nt][0] = *reinterpret_cast<const float4 *>(sf + static_cast<size_t>(g0) * Npad + nb0);
+                    sfl[i][nt][1] = *reinterpret_cast<const float4 *>(sf + static_cast<size_t>(g1) * Npad + nb0);
+                }
             }
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
@@ -1344,20 +1378,52 @@ wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
         // Keep the scheduler from sinking the loads back next to their MFMAs (it does so to cut
         // register pressure, which turns the round into one serial latency per fragment).
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (EXACT) {
 #pragma unroll
-        for (int i = 0; i < kDepth; ++i) {
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
+            for (int i = 0; i < kDepth; ++i) {
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt) {
-                    const uint32_t szv = static_cast<uint32_t>(
-                        __builtin_amdgcn_ds_bpermute(((lane & 15) + 16 * t) * 4, static_cast<int>(szl[i][nt])));
-                    half2_t nz, sc;
-                    split_sz(szv, nz, sc);
-                    const half8_t a = dequant_frag<BITS>(w[i][nt], t, nz, sc);
+                    float4_t tacc[MT];
 #pragma unroll
-                    for (int mt = 0; mt < MT; ++mt)
-                        acc[nt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, xb[i][t][mt], acc[nt][mt], 0, 0, 0);
+                    for (int t = 0; t < 4; ++t) {
+                        const uint32_t szv = static_cast<uint32_t>(
+                            __builtin_amdgcn_ds_bpermute(((lane & 15) + 16 * t) * 4, static_cast<int>(szl[i][nt])));
+                        const half2_t p = __builtin_bit_cast(half2_t, szv);
+                        const half8_t a = dequant_exact<BITS>(w[i][nt], t, exact_consts(half2_t{p[0], p[0]}));
+                        const bool first = t == 0 || (t == 2 && g64);
+#pragma unroll
+                        for (int mt = 0; mt < MT; ++mt)
+                            tacc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                                a, xb[i][t][mt], first ? float4_t{0.f, 0.f, 0.f, 0.f} : tacc[mt], 0, 0, 0);
+                        if (t == 3 || (t == 1 && g64)) {
+                            const float4 sv = sfl[i][nt][t == 3 && g64 ? 1 : 0];
+#pragma unroll
+                            for (int mt = 0; mt < MT; ++mt) {
+                                acc[nt][mt][0] = __builtin_fmaf(sv.x, tacc[mt][0], acc[nt][mt][0]);
+                                acc[nt][mt][1] = __builtin_fmaf(sv.y, tacc[mt][1], acc[nt][mt][1]);
+                                acc[nt][mt][2] = __builtin_fmaf(sv.z, tacc[mt][2], acc[nt][mt][2]);
+                                acc[nt][mt][3] = __builtin_fmaf(sv.w, tacc[mt][3], acc[nt][mt][3]);
+                            }
+                        }
+                    }
+                }
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < kDepth; ++i) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt) {
+                        const uint32_t szv = static_cast<uint32_t>(
+                            __builtin_amdgcn_ds_bpermute(((lane & 15) + 16 * t) * 4, static_cast<int>(szl[i][nt])));
+                        half2_t nz, sc;
+                        split_sz(szv, nz, sc);
+                        const half8_t a = dequant_frag<BITS>(w[i][nt], t, nz, sc);
+#pragma unroll
+                        for (int mt = 0; mt < MT; ++mt)
+                            acc[nt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, xb[i][t][mt], acc[nt][mt], 0, 0, 0);
+                    }
                 }
             }
         }
@@ -1403,8 +1469,13 @@ wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
 
 constexpr int kDecodeMaxM = 64;
 
-// Decode tile policy: (NT, nsplit) per M bucket, chosen from the M-sweep;
-// h->dcfg (measurement knob) overrides it: dcfg = 16 * log2(NT) + log2(nsplit) + 1.
+// Exact-weight kernels apply when the group tiles K (a stage never straddles two groups).
+inline bool use_exact(const dllm_linear *h) {
+    return h->precision == DLLM_PRECISION_EXACT &&
+           exact_gemm_supported(1, static_cast<int>(h->K), static_cast<int>(h->Npad), static_cast<int>(h->group));
+}
+
+// Decode tile policy: (NT, nsplit) per M bucket, chosen from the M-sweep.
 // Measured (scripts/decode_sweep.py, 48-layer graph, K = N = 4096 int4, us per layer;
 // profiles/r01_decode_tiles): up to M = 32 the one-tile kernel wins (M 1/16/32: 5.1/6.9/10.7;
 // the slab combine's extra launch costs ~4.7 us and NT = 4 without a split leaves 64 blocks whose
@@ -1414,7 +1485,7 @@ inline void decode_policy(int M, int &nt, int &nsplit) {
     nt = nsplit = M > 32 ? 4 : 1;
 }
 
-template <int BITS, typename YT, int MT, int NT>
+template <int BITS, typename YT, int MT, int NT, bool EXACT>
 int launch_decode_nt(const dllm_linear *h, const __half *X, int M, YT *Y, int nsplit, hipStream_t st) {
     const unsigned nbx = static_cast<unsigned>(h->Npad / (16 * NT));
     const int K = static_cast<int>(h->K), N = static_cast<int>(h->N);
@@ -1422,14 +1493,15 @@ int launch_decode_nt(const dllm_linear *h, const __half *X, int M, YT *Y, int ns
     const int nslab = (K + 127) / 128;
     nsplit = std::max(1, std::min(nsplit, nslab));
     if (nsplit == 1) {
-        wq_decode_kernel<BITS, YT, MT, NT><<<nbx, kDecWaves * 64, 0, st>>>(X, M, K, h->wdec, h->sz, h->bias, Y, N, Np, gr);
+        wq_decode_kernel<BITS, YT, MT, NT, false, 0, EXACT><<<nbx, kDecWaves * 64, 0, st>>>(
+            X, M, K, h->wdec, h->sz, h->bias, Y, N, Np, gr, 1, nullptr, h->sf);
         DLLM_LAUNCH_CHECK();
         return DLLM_OK;
     }
     float *ws = device_workspace(st, static_cast<size_t>(nsplit) * M * h->Npad * sizeof(float));
     if (!ws) return DLLM_ERR_HIP;
-    wq_decode_kernel<BITS, YT, MT, NT, true><<<dim3(nbx, static_cast<unsigned>(nsplit)), kDecWaves * 64, 0, st>>>(
-        X, M, K, h->wdec, h->sz, h->bias, Y, N, Np, gr, nsplit, ws);
+    wq_decode_kernel<BITS, YT, MT, NT, true, 0, EXACT><<<dim3(nbx, static_cast<unsigned>(nsplit)), kDecWaves * 64, 0, st>>>(
+        X, M, K, h->wdec, h->sz, h->bias, Y, N, Np, gr, nsplit, ws, h->sf);
     DLLM_LAUNCH_CHECK();
     const size_t q = static_cast<size_t>(M) * (h->Npad / 4);
     const unsigned rb = static_cast<unsigned>(std::min<size_t>((q + 255) / 256, 4 * kCUs));
@@ -1438,44 +1510,104 @@ int launch_decode_nt(const dllm_linear *h, const __half *X, int M, YT *Y, int ns
     return DLLM_OK;
 }
 
-template <int BITS, typename YT, int MT>
+template <int BITS, typename YT, int MT, bool EXACT>
 int launch_decode_mt(const dllm_linear *h, const __half *X, int M, YT *Y, int nt, int nsplit, hipStream_t st) {
     switch (nt) {
-    case 2: return launch_decode_nt<BITS, YT, MT, 2>(h, X, M, Y, nsplit, st);
-    case 4: return launch_decode_nt<BITS, YT, MT, 4>(h, X, M, Y, nsplit, st);
-    default: return launch_decode_nt<BITS, YT, MT, 1>(h, X, M, Y, nsplit, st);
+    case 2: return launch_decode_nt<BITS, YT, MT, 2, EXACT>(h, X, M, Y, nsplit, st);
+    case 4: return launch_decode_nt<BITS, YT, MT, 4, EXACT>(h, X, M, Y, nsplit, st);
+    default: return launch_decode_nt<BITS, YT, MT, 1, EXACT>(h, X, M, Y, nsplit, st);
     }
 }
 
+template <int BITS, typename YT, bool EXACT>
+int launch_decode_x(const dllm_linear *h, const __half *X, size_t M, YT *Y, int nt, int nsplit, hipStream_t st) {
+    const int Mi = static_cast<int>(M);
+    if (M <= 16) return launch_decode_mt<BITS, YT, 1, EXACT>(h, X, Mi, Y, nt, nsplit, st);
+    if (M <= 32) return launch_decode_mt<BITS, YT, 2, EXACT>(h, X, Mi, Y, nt, nsplit, st);
+    return launch_decode_mt<BITS, YT, 4, EXACT>(h, X, Mi, Y, nt, nsplit, st);
+}
+
+#if DLLM_LAB
 template <int BITS, typename YT>
-int launch_decode(const dllm_linear *h, const __half *X, size_t M, YT *Y, hipStream_t st) {
+int launch_decode_lab(const dllm_linear *h, const __half *X, size_t M, YT *Y, hipStream_t st) {
     const unsigned nb = static_cast<unsigned>(h->Npad / 16);
     const int Mi = static_cast<int>(M), K = static_cast<int>(h->K), N = static_cast<int>(h->N);
     const int Np = static_cast<int>(h->Npad), gr = static_cast<int>(h->group);
-    if (M <= 16 && h->dlab != 0) {
-        switch (h->dlab) {
+    switch (h->dlab) {
 #define DLLM_DLAB(L) case L: wq_decode_kernel<BITS, YT, 1, 1, false, L><<<nb, kDecWaves * 64, 0, st>>>(X, Mi, K, h->wdec, h->sz, h->bias, Y, N, Np, gr); break;
-            DLLM_DLAB(1) DLLM_DLAB(2) DLLM_DLAB(3) DLLM_DLAB(4) DLLM_DLAB(5) DLLM_DLAB(6) DLLM_DLAB(7)
+        DLLM_DLAB(1) DLLM_DLAB(2) DLLM_DLAB(3) DLLM_DLAB(4) DLLM_DLAB(5) DLLM_DLAB(6) DLLM_DLAB(7)
 #undef DLLM_DLAB
+        default: break;
+    }
+    DLLM_LAUNCH_CHECK();
+    return DLLM_OK;
+}
+#endif
+
+template <int BITS, typename YT>
+int launch_decode(const dllm_linear *h, const __half *X, size_t M, YT *Y, hipStream_t st) {
+    int nt, nsplit;
+    decode_policy(static_cast<int>(M), nt, nsplit);
+#if DLLM_LAB
+    if (M <= 16 && h->dlab != 0) return launch_decode_lab<BITS, YT>(h, X, M, Y, st);
+    if (h->dcfg > 0) {   // dcfg = 16 log2(NT) + log2(nsplit) + 1
+        nt = 1 << ((h->dcfg - 1) / 16);
+        nsplit = 1 << ((h->dcfg - 1) % 16);
+    }
+#endif
+    // the column group must tile Npad (a multiple of 128)
+    while (nt > 1 && h->Npad % (16 * nt)) nt /= 2;
+    if (use_exact(h)) return launch_decode_x<BITS, YT, true>(h, X, M, Y, nt, nsplit, st);
+    return launch_decode_x<BITS, YT, false>(h, X, M, Y, nt, nsplit, st);
+}
+
+// 3-stage-ring GEMM (rounded weights) with tile (32 MR) x (32 NW), K optionally split into nsplit slices.
+template <int BITS, typename YT, int NW, int MR, int KG = 1, int EPI = 0>
+int launch_ring(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t st, int nsplit,
+                const PSampleEpi *epi = nullptr) {
+    const int nbm = (M + 32 * MR - 1) / (32 * MR), nbn = static_cast<int>(h->Npad / (32 * NW));
+    const unsigned nb = static_cast<unsigned>(nbm * nbn * nsplit);
+    const PSampleEpi ep = epi ? *epi : PSampleEpi{};
+#if DLLM_LAB
+    if (EPI == 0 && h->rlab != 0 && nsplit == 1) {   // measurement only
+        switch (h->rlab) {
+#define DLLM_RLAB(L)                                                                                              \
+    case L:                                                                                                       \
+        wq_gemm8_kernel<BITS, YT, NW, MR, false, KG, L><<<nb, NW * KG * 64, 0, st>>>(                           \
+            X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn);   \
+        break;
+            DLLM_RLAB(1) DLLM_RLAB(2) DLLM_RLAB(3) DLLM_RLAB(4) DLLM_RLAB(5) DLLM_RLAB(6) DLLM_RLAB(7)
+            DLLM_RLAB(8) DLLM_RLAB(9) DLLM_RLAB(10) DLLM_RLAB(11) DLLM_RLAB(16) DLLM_RLAB(20) DLLM_RLAB(32)
+            DLLM_RLAB(40)
+#undef DLLM_RLAB
             default: break;
         }
         DLLM_LAUNCH_CHECK();
         return DLLM_OK;
     }
-    int nt, nsplit;
-    if (h->dcfg > 0) {
-        nt = 1 << ((h->dcfg - 1) / 16);
-        nsplit = 1 << ((h->dcfg - 1) % 16);
-    } else {
-        decode_policy(Mi, nt, nsplit);
+#endif
+    if (nsplit == 1) {
+        wq_gemm8_kernel<BITS, YT, NW, MR, false, KG, 0, EPI><<<nb, NW * KG * 64, 0, st>>>(
+            X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn, 1,
+            nullptr, ep);
+        DLLM_LAUNCH_CHECK();
+        return DLLM_OK;
     }
-    // the column group must tile Npad (a multiple of 128)
-    while (nt > 1 && h->Npad % (16 * nt)) nt /= 2;
-    if (M <= 16) return launch_decode_mt<BITS, YT, 1>(h, X, Mi, Y, nt, nsplit, st);
-    if (M <= 32) return launch_decode_mt<BITS, YT, 2>(h, X, Mi, Y, nt, nsplit, st);
-    return launch_decode_mt<BITS, YT, 4>(h, X, Mi, Y, nt, nsplit, st);
+    float *ws = device_workspace(st, static_cast<size_t>(nsplit) * M * h->Npad * sizeof(float));
+    if (!ws) return DLLM_ERR_HIP;
+    wq_gemm8_kernel<BITS, YT, NW, MR, true, KG><<<nb, NW * KG * 64, 0, st>>>(
+        X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn, nsplit, ws);
+    DLLM_LAUNCH_CHECK();
+    const size_t q = static_cast<size_t>(M) * (h->Npad / 4);
+    const unsigned rb = static_cast<unsigned>(std::min<size_t>((q + 255) / 256, 4 * kCUs));
+    splitk_reduce_kernel<YT, EPI><<<rb, 256, 0, st>>>(ws, nsplit, M, (int)h->N, (int)h->Npad, h->bias, Y, ep);
+    DLLM_LAUNCH_CHECK();
+    return DLLM_OK;
 }
 
+#if DLLM_LAB
+// Lab schedules (variants 0..3 and 5..13; see dllm_linear_set_kernel_variant).  Returns -1 when
+// the variant does not apply to this shape (the product policy runs instead).
 template <int BITS, typename YT, int VAR>
 void launch_prefill(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t st) {
     const int nbm = (M + kBM - 1) / kBM, nbn = static_cast<int>(h->Npad / kBN);
@@ -1484,8 +1616,6 @@ void launch_prefill(const dllm_linear *h, const __half *X, int M, YT *Y, hipStre
                                                            (int)h->Npad, (int)h->group, nbm, nbn);
 }
 
-// Mid-M prefill (too few 256-row tiles to fill 256 CUs): 128-row tiles, and when even those are
-// too few, K split into nsplit slices (slab partials + splitk_reduce_kernel).
 template <int BITS, typename YT>
 int launch_mid(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t st) {
     constexpr int MR = 4;
@@ -1513,115 +1643,111 @@ int launch_mid(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t 
     return DLLM_OK;
 }
 
-// 3-stage-ring GEMM with tile (32 MR) x (32 NW), K optionally split into nsplit slices.
-template <int BITS, typename YT, int NW, int MR, int KG = 1, int EPI = 0>
-int launch_ring(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t st, int nsplit,
-                const PSampleEpi *epi = nullptr) {
-    const int nbm = (M + 32 * MR - 1) / (32 * MR), nbn = static_cast<int>(h->Npad / (32 * NW));
-    const unsigned nb = static_cast<unsigned>(nbm * nbn * nsplit);
+template <int BITS, typename YT, int EPI>
+int launch_lab_variant(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t st, const PSampleEpi *epi) {
+    const int np = static_cast<int>(h->Npad);
+    const int mb256 = (M + 255) / 256, mb128 = (M + 127) / 128;
     const PSampleEpi ep = epi ? *epi : PSampleEpi{};
-    if (EPI == 0 && h->rlab != 0 && nsplit == 1) {   // measurement only
-        switch (h->rlab) {
-#define DLLM_RLAB(L)                                                                                              \
-    case L:                                                                                                       \
-        wq_gemm8_kernel<BITS, YT, NW, MR, false, KG, L><<<nb, NW * KG * 64, 0, st>>>(                           \
-            X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn);   \
-        break;
-            DLLM_RLAB(1) DLLM_RLAB(2) DLLM_RLAB(3) DLLM_RLAB(4) DLLM_RLAB(5) DLLM_RLAB(6) DLLM_RLAB(7)
-            DLLM_RLAB(8) DLLM_RLAB(9) DLLM_RLAB(10) DLLM_RLAB(11) DLLM_RLAB(16) DLLM_RLAB(20) DLLM_RLAB(32)
-            DLLM_RLAB(40)
-#undef DLLM_RLAB
-            default: break;
+    const int v = h->variant;
+    if (EPI == 0 && v >= 0 && v <= 3) {
+        switch (v) {
+        case 0: launch_prefill<BITS, YT, 0>(h, X, M, Y, st); break;
+        case 1: launch_prefill<BITS, YT, 1>(h, X, M, Y, st); break;
+        case 2: launch_prefill<BITS, YT, 2>(h, X, M, Y, st); break;
+        default: launch_prefill<BITS, YT, 3>(h, X, M, Y, st); break;
         }
         DLLM_LAUNCH_CHECK();
         return DLLM_OK;
     }
-    if (nsplit == 1) {
-        wq_gemm8_kernel<BITS, YT, NW, MR, false, KG, 0, EPI><<<nb, NW * KG * 64, 0, st>>>(
-            X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn, 1,
-            nullptr, ep);
+    if (EPI == 0 && v == 6) {
+        const int tiles256 = mb256 * static_cast<int>(h->Npad / kBN);
+        if (tiles256 < kCUs) return launch_mid<BITS, YT>(h, X, M, Y, st);
+        launch_prefill<BITS, YT, 3>(h, X, M, Y, st);
         DLLM_LAUNCH_CHECK();
         return DLLM_OK;
     }
-    float *ws = device_workspace(st, static_cast<size_t>(nsplit) * M * h->Npad * sizeof(float));
-    if (!ws) return DLLM_ERR_HIP;
-    wq_gemm8_kernel<BITS, YT, NW, MR, true, KG><<<nb, NW * KG * 64, 0, st>>>(
-        X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn, nsplit, ws);
-    DLLM_LAUNCH_CHECK();
-    const size_t q = static_cast<size_t>(M) * (h->Npad / 4);
-    const unsigned rb = static_cast<unsigned>(std::min<size_t>((q + 255) / 256, 4 * kCUs));
-    splitk_reduce_kernel<YT, EPI><<<rb, 256, 0, st>>>(ws, nsplit, M, (int)h->N, (int)h->Npad, h->bias, Y, ep);
-    DLLM_LAUNCH_CHECK();
-    return DLLM_OK;
-}
-
-// Tile policy (variant 4, the default): the largest tile that still gives >= 256 blocks; below
-// that, 128 x 128 tiles with K split until ~200+ blocks (slab partials + ordered combine).
-template <int BITS, typename YT, int EPI = 0>
-int launch_auto(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t st,
-                const PSampleEpi *epi = nullptr) {
-    const int np = static_cast<int>(h->Npad);
-    const int mb256 = (M + 255) / 256, mb128 = (M + 127) / 128;
-    if (h->variant == 12 && np % 256 == 0 && mb128 * (np / 256) >= kCUs)   // 128 x 256 tiles (A/B)
-        return launch_ring<BITS, YT, 8, 4, 1, EPI>(h, X, M, Y, st, 1, epi);
+    if (v == 12 && np % 256 == 0 && mb128 * (np / 256) >= kCUs) return launch_ring<BITS, YT, 8, 4, 1, EPI>(h, X, M, Y, st, 1, epi);
     if (np % 256 == 0 && mb256 * (np / 256) >= kCUs) {
-        if (h->variant >= 9 && h->variant <= 11)   // ping-pong schedules (linear_pp.hip)
+        if (v >= 9 && v <= 11)   // ping-pong schedules (linear_pp.hip)
             return launch_pp_gemm(BITS, std::is_same<YT, float>::value ? 1 : 0, X, M, (int)h->K,
-                                  h->variant == 11 ? h->w16 : h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad,
-                                  (int)h->group, h->variant - 8, EPI ? epi : nullptr, st, h->pplab);
-        if (h->variant == 8) {
-            const PSampleEpi ep = epi ? *epi : PSampleEpi{};
+                                  v == 11 ? h->w16 : h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad,
+                                  (int)h->group, v - 8, EPI ? epi : nullptr, st, h->pplab);
+        if (v == 8) {
             wq_gemm16_kernel<BITS, YT, EPI><<<static_cast<unsigned>(mb256 * (np / 256)), 512, 0, st>>>(
                 X, M, (int)h->K, h->w16, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, mb256, np / 256, ep);
             DLLM_LAUNCH_CHECK();
             return DLLM_OK;
         }
-        if (h->variant == 7) {
-            const PSampleEpi ep = epi ? *epi : PSampleEpi{};
+        if (v == 7) {
             wq_gemm_w2_kernel<BITS, YT, false, EPI><<<static_cast<unsigned>(mb256 * (np / 256)), 512, 0, st>>>(
                 X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, mb256, np / 256,
                 1, nullptr, ep);
             DLLM_LAUNCH_CHECK();
             return DLLM_OK;
         }
-        return launch_ring<BITS, YT, 8, 8, 1, EPI>(h, X, M, Y, st, 1, epi);
     }
-    if (h->variant == 13 && np % 256 == 0 && 2 * mb256 * (np / 256) >= kCUs && (h->K / kBK) % 2 == 0)
-        return launch_ring<BITS, YT, 8, 8, 1, EPI>(h, X, M, Y, st, 2, epi);   // 256 x 256, K split 2 (A/B)
-    const bool kg2 = h->variant != 5;   // variant 5: the same tiles with one k-group (A/B)
-    if (mb256 * (np / 128) >= kCUs)
-        return kg2 ? launch_ring<BITS, YT, 4, 8, 2, EPI>(h, X, M, Y, st, 1, epi)
-                   : launch_ring<BITS, YT, 4, 8, 1, EPI>(h, X, M, Y, st, 1, epi);
+    if (v == 13 && np % 256 == 0 && 2 * mb256 * (np / 256) >= kCUs && (h->K / kBK) % 2 == 0)
+        return launch_ring<BITS, YT, 8, 8, 1, EPI>(h, X, M, Y, st, 2, epi);   // 256 x 256, K split 2
+    if (v == 5 && !(np % 256 == 0 && mb256 * (np / 256) >= kCUs) && mb256 * (np / 128) >= kCUs)
+        return launch_ring<BITS, YT, 4, 8, 1, EPI>(h, X, M, Y, st, 1, epi);   // one k-group
+    return -1;
+}
+#endif  // DLLM_LAB
+
+// Rounded-weight (DLLM_PRECISION_F16W) tile policy: the largest tile that still gives >= 256
+// blocks -- 256 x 256 (8 waves), 256 x 128 (8 waves, two k-groups) -- below that 128 x 128 tiles
+// (two k-groups) with K split until ~200+ blocks (slab partials + ordered combine).
+template <int BITS, typename YT, int EPI = 0>
+int launch_rounded(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t st,
+                   const PSampleEpi *epi = nullptr) {
+    const int np = static_cast<int>(h->Npad);
+    const int mb256 = (M + 255) / 256, mb128 = (M + 127) / 128;
+    if (np % 256 == 0 && mb256 * (np / 256) >= kCUs) return launch_ring<BITS, YT, 8, 8, 1, EPI>(h, X, M, Y, st, 1, epi);
+    if (mb256 * (np / 128) >= kCUs) return launch_ring<BITS, YT, 4, 8, 2, EPI>(h, X, M, Y, st, 1, epi);
     const int tiles = mb128 * (np / 128);
     const int nk = static_cast<int>(h->K / kBK);
     int nsplit = 1;
     while (tiles * nsplit < 200 && nsplit < 8 && nk % (2 * nsplit) == 0 && nk / (2 * nsplit) >= 4) nsplit *= 2;
-    return kg2 ? launch_ring<BITS, YT, 4, 4, 2, EPI>(h, X, M, Y, st, nsplit, epi)
-               : launch_ring<BITS, YT, 4, 4, 1, EPI>(h, X, M, Y, st, nsplit, epi);
+    return launch_ring<BITS, YT, 4, 4, 2, EPI>(h, X, M, Y, st, nsplit, epi);
+}
+
+inline ExactGemmArgs exact_args(const dllm_linear *h, const __half *X, int M, void *Y, const PSampleEpi *epi) {
+    ExactGemmArgs a{h->bits, X, M, (int)h->K, h->wdev, h->sz, h->sf, h->bias, Y, (int)h->N, (int)h->Npad,
+                    (int)h->group, epi};
+#if DLLM_LAB
+    a.tm = h->variant == 15 ? 1 : 0;
+#endif
+    return a;
+}
+
+// Prefill (M > kDecodeMaxM) dispatch: exact-weight kernels (default precision) or the rounded ring.
+template <int BITS, typename YT, int EPI = 0>
+int launch_prefill_auto(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t st,
+                        const PSampleEpi *epi = nullptr) {
+#if DLLM_LAB
+    // lab A/B: 4 = the rounded policy, 14 / 15 = exact (128 x 256 / tile-major 256 x 256), others
+    // = the round-1 schedules; -1 (default) = the product policy below
+    if (h->variant == 4) return launch_rounded<BITS, YT, EPI>(h, X, M, Y, st, epi);
+    if ((h->variant == 14 || h->variant == 15) && exact_gemm_supported(M, (int)h->K, (int)h->Npad, (int)h->group))
+        return launch_exact_gemm(exact_args(h, X, M, Y, epi), std::is_same<YT, float>::value ? 1 : 0, st);
+    if (h->variant >= 0) {
+        const int rc = launch_lab_variant<BITS, YT, EPI>(h, X, M, Y, st, epi);
+        if (rc >= 0) return rc;
+    }
+#endif
+    if (use_exact(h)) return launch_exact_gemm(exact_args(h, X, M, Y, epi), std::is_same<YT, float>::value ? 1 : 0, st);
+    return launch_rounded<BITS, YT, EPI>(h, X, M, Y, st, epi);
 }
 
 template <int BITS, typename YT>
 int launch_gemm_t(const dllm_linear *h, const __half *X, size_t M, YT *Y, hipStream_t st) {
     if (M <= static_cast<size_t>(kDecodeMaxM)) return launch_decode<BITS, YT>(h, X, M, Y, st);
-    if (h->variant == 4 || h->variant == 5 || h->variant >= 7)
-        return launch_auto<BITS, YT>(h, X, (int)M, Y, st);
-    if (h->variant == 6) {   // previous policy: 2-stage kernels, 128-row tiles + split below 256 tiles
-        const int tiles256 = static_cast<int>((M + kBM - 1) / kBM) * static_cast<int>(h->Npad / kBN);
-        if (tiles256 < kCUs) return launch_mid<BITS, YT>(h, X, (int)M, Y, st);
-    }
-    switch (h->variant) {
-    case 0: launch_prefill<BITS, YT, 0>(h, X, (int)M, Y, st); break;
-    case 1: launch_prefill<BITS, YT, 1>(h, X, (int)M, Y, st); break;
-    case 2: launch_prefill<BITS, YT, 2>(h, X, (int)M, Y, st); break;
-    default: launch_prefill<BITS, YT, 3>(h, X, (int)M, Y, st); break;
-    }
-    DLLM_LAUNCH_CHECK();
-    return DLLM_OK;
+    return launch_prefill_auto<BITS, YT>(h, X, static_cast<int>(M), Y, st);
 }
 
 template <int BITS>
 int psample_fused(dllm_linear *h, const __half *Xh, int M, const PSampleEpi &ep, hipStream_t st) {
-    return launch_auto<BITS, float, 1>(h, Xh, M, ep.x_prev, st, &ep);
+    return launch_prefill_auto<BITS, float, 1>(h, Xh, M, ep.x_prev, st, &ep);
 }
 
 template <int BITS>
@@ -1632,25 +1758,30 @@ int launch_gemm(const dllm_linear *h, const __half *X, size_t M, void *Y, int y_
 
 void free_linear(dllm_linear *h) {
     if (!h) return;
-    (void)hipFree(h->wdev); (void)hipFree(h->wdec); (void)hipFree(h->w16); (void)hipFree(h->sz); (void)hipFree(h->canon); (void)hipFree(h->scales);
-    (void)hipFree(h->zps); (void)hipFree(h->bias); (void)hipFree(h->xws);
+    (void)hipFree(h->wdev); (void)hipFree(h->wdec); (void)hipFree(h->sz); (void)hipFree(h->sf);
+    (void)hipFree(h->scales); (void)hipFree(h->zps); (void)hipFree(h->bias); (void)hipFree(h->xws);
+#if DLLM_LAB
+    (void)hipFree(h->w16);
+#endif
     delete h;
 }
 
-int check_shape(size_t K, size_t N, uint8_t bits, size_t group) {
+int check_shape(size_t K, size_t N, uint8_t bits, size_t group, int precision) {
     if (bits != 2 && bits != 4 && bits != 8)
         return fail(DLLM_ERR_UNSUPPORTED, "linear layer supports bits in {2, 4, 8}");
     if (K == 0 || N == 0) return fail(DLLM_ERR_SHAPE_MISMATCH, "K and N must be >= 1");
     if (K % kBK) return fail(DLLM_ERR_SHAPE_MISMATCH, "K must be a multiple of 64");
     if (group == 0 || group % kBK) return fail(DLLM_ERR_INVALID_PARAMS, "group must be a positive multiple of 64");
     if (K > (1u << 30) || N > (1u << 30)) return fail(DLLM_ERR_SHAPE_MISMATCH, "dimension too large");
+    if (precision != DLLM_PRECISION_EXACT && precision != DLLM_PRECISION_F16W)
+        return fail(DLLM_ERR_INVALID_PARAMS, "precision must be DLLM_PRECISION_EXACT or DLLM_PRECISION_F16W");
     return DLLM_OK;
 }
 
-int alloc_linear(size_t K, size_t N, uint8_t bits, size_t group, dllm_linear **out) {
+int alloc_linear(size_t K, size_t N, uint8_t bits, size_t group, int precision, dllm_linear **out) {
     dllm_linear *h = new (std::nothrow) dllm_linear();
     if (!h) return fail(DLLM_ERR_HIP, "out of host memory");
-    h->K = K; h->N = N; h->bits = bits; h->group = group;
+    h->K = K; h->N = N; h->bits = bits; h->group = group; h->precision = precision;
     h->Npad = (N + kBN - 1) / kBN * kBN;
     h->G = (K + group - 1) / group;
     (void)hipGetDevice(&h->device);
@@ -1658,12 +1789,14 @@ int alloc_linear(size_t K, size_t N, uint8_t bits, size_t group, dllm_linear **o
     hipError_t e = hipSuccess;
     if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->wdev), h->Npad * K * bits / 8);
     if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->wdec), h->Npad * ((K + 127) / 128) * 128 * bits / 8);
-    if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->w16), h->Npad * K * bits / 8);
     if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->sz), h->G * h->Npad * 4);
-    if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->canon), canon_words(K, N, bits) * 4);
+    if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->sf), h->G * h->Npad * 4);
     if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->scales), h->G * N * 4);
     if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->zps), h->G * N);
     if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->bias), h->Npad * 4);
+#if DLLM_LAB
+    if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->w16), h->Npad * K * bits / 8);
+#endif
     if (e != hipSuccess) {
         free_linear(h);
         return fail(DLLM_ERR_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
@@ -1672,19 +1805,25 @@ int alloc_linear(size_t K, size_t N, uint8_t bits, size_t group, dllm_linear **o
     return DLLM_OK;
 }
 
-int finish_linear(dllm_linear *h, const float *bias, hipStream_t st) {
+// Device layouts from the canonical codes (`canon`, u32-addressable, ceil(K N bits / 32) words)
+// and the scales / zero points already in the handle.  `canon` is only read by these launches.
+int finish_linear(dllm_linear *h, const uint32_t *canon, const float *bias, hipStream_t st) {
     DLLM_HIP_TRY(hipMemsetAsync(h->bias, 0, h->Npad * 4, st));
     if (bias) DLLM_HIP_TRY(hipMemcpyAsync(h->bias, bias, h->N * 4, hipMemcpyDeviceToDevice, st));
     dim3 gf(static_cast<unsigned>((h->Npad + 255) / 256), static_cast<unsigned>(h->K / 64));
-    build_fragments_kernel<<<gf, 256, 0, st>>>(h->canon, h->K, h->N, h->Npad, h->bits, h->wdev);
+    build_fragments_kernel<<<gf, 256, 0, st>>>(canon, h->K, h->N, h->Npad, h->bits, h->wdev);
     DLLM_LAUNCH_CHECK();
-    build_fragments16_kernel<<<gf, 256, 0, st>>>(h->canon, h->K, h->N, h->Npad, h->bits, h->w16);
+#if DLLM_LAB
+    build_fragments16_kernel<<<gf, 256, 0, st>>>(canon, h->K, h->N, h->Npad, h->bits, h->w16);
     DLLM_LAUNCH_CHECK();
+#endif
     dim3 gd(static_cast<unsigned>((h->Npad + 255) / 256), static_cast<unsigned>((h->K + 127) / 128));
-    build_decode_kernel<<<gd, 256, 0, st>>>(h->canon, h->K, h->N, h->Npad, h->bits, h->wdec);
+    build_decode_kernel<<<gd, 256, 0, st>>>(canon, h->K, h->N, h->Npad, h->bits, h->wdec);
     DLLM_LAUNCH_CHECK();
     dim3 gs(static_cast<unsigned>((h->Npad + 255) / 256), static_cast<unsigned>(h->G));
     build_sz_kernel<<<gs, 256, 0, st>>>(h->scales, h->zps, h->G, h->N, h->Npad, h->sz);
+    DLLM_LAUNCH_CHECK();
+    build_sf_kernel<<<gs, 256, 0, st>>>(h->scales, h->G, h->N, h->Npad, h->sf);
     DLLM_LAUNCH_CHECK();
     return DLLM_OK;
 }
@@ -1696,28 +1835,59 @@ using namespace dllm;
 
 extern "C" {
 
-int dllm_linear_create(const float *W, const float *bias, size_t K, size_t N, uint8_t bits, size_t group,
-                       dllm_linear_t *out, dllm_stream_t stream) {
+int dllm_linear_create_ex(const float *W, const float *bias, size_t K, size_t N, uint8_t bits, size_t group,
+                          int precision, dllm_linear_t *out, dllm_stream_t stream) {
     if (!out || !W) return fail(DLLM_ERR_INVALID_PARAMS, "null pointer");
-    int rc = check_shape(K, N, bits, group);
+    int rc = check_shape(K, N, bits, group, precision);
     if (rc) return rc;
     dllm_linear *h = nullptr;
-    if ((rc = alloc_linear(K, N, bits, group, &h))) return rc;
+    if ((rc = alloc_linear(K, N, bits, group, precision, &h))) return rc;
     hipStream_t st = as_stream(stream);
-    hipError_t e = hipMemsetAsync(h->canon, 0, canon_words(K, N, bits) * 4, st);
+    // The canonical codes only live for the creation: a per-stream workspace slot (reused by every
+    // create on this stream, in stream order), not handle memory.
+    const size_t cbytes = canon_words(K, N, bits) * 4;
+    uint32_t *canon = reinterpret_cast<uint32_t *>(device_workspace(st, cbytes, 3));
+    if (!canon) { free_linear(h); return DLLM_ERR_HIP; }
+    hipError_t e = hipMemsetAsync(canon, 0, cbytes, st);
     if (e != hipSuccess) { free_linear(h); return fail(DLLM_ERR_HIP, hipGetErrorString(e)); }
     if (N % 4 == 0 && group <= 128 && (bits == 2 || bits == 4 || bits == 8) &&
         (reinterpret_cast<uintptr_t>(W) & 15) == 0) {
         dim3 g(static_cast<unsigned>((N + 255) / 256), static_cast<unsigned>(h->G));
-        quantize_weights4_kernel<<<g, 256, 0, st>>>(W, K, N, bits, static_cast<int>(group), h->canon, h->scales,
-                                                     h->zps);
+        quantize_weights4_kernel<<<g, 256, 0, st>>>(W, K, N, bits, static_cast<int>(group), canon, h->scales, h->zps);
     } else {
         dim3 g(static_cast<unsigned>((N + 255) / 256), static_cast<unsigned>(h->G));
-        quantize_weights_kernel<<<g, 256, 0, st>>>(W, K, N, bits, static_cast<int>(group), h->canon, h->scales,
-                                                    h->zps);
+        quantize_weights_kernel<<<g, 256, 0, st>>>(W, K, N, bits, static_cast<int>(group), canon, h->scales, h->zps);
     }
     if (hipGetLastError() != hipSuccess) { free_linear(h); return fail(DLLM_ERR_HIP, "quantize_weights launch"); }
-    if ((rc = finish_linear(h, bias, st))) { free_linear(h); return rc; }
+    if ((rc = finish_linear(h, canon, bias, st))) { free_linear(h); return rc; }
+    *out = h;
+    return DLLM_OK;
+}
+
+int dllm_linear_create(const float *W, const float *bias, size_t K, size_t N, uint8_t bits, size_t group,
+                       dllm_linear_t *out, dllm_stream_t stream) {
+    return dllm_linear_create_ex(W, bias, K, N, bits, group, DLLM_PRECISION_EXACT, out, stream);
+}
+
+int dllm_linear_create_quantized_ex(const uint8_t *packed_codes, const float *scales, const uint8_t *zps,
+                                    const float *bias, size_t K, size_t N, uint8_t bits, size_t group, int precision,
+                                    dllm_linear_t *out, dllm_stream_t stream) {
+    if (!out || !packed_codes || !scales || !zps) return fail(DLLM_ERR_INVALID_PARAMS, "null pointer");
+    int rc = check_shape(K, N, bits, group, precision);
+    if (rc) return rc;
+    dllm_linear *h = nullptr;
+    if ((rc = alloc_linear(K, N, bits, group, precision, &h))) return rc;
+    hipStream_t st = as_stream(stream);
+    // The caller's bitstream is read through u32 words: stage it in a zero-padded workspace.
+    const size_t nbytes = (K * N * bits + 7) / 8, cbytes = canon_words(K, N, bits) * 4;
+    uint32_t *canon = reinterpret_cast<uint32_t *>(device_workspace(st, cbytes, 3));
+    if (!canon) { free_linear(h); return DLLM_ERR_HIP; }
+    hipError_t e = hipMemsetAsync(canon, 0, cbytes, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(canon, packed_codes, nbytes, hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(h->scales, scales, h->G * N * 4, hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(h->zps, zps, h->G * N, hipMemcpyDeviceToDevice, st);
+    if (e != hipSuccess) { free_linear(h); return fail(DLLM_ERR_HIP, hipGetErrorString(e)); }
+    if ((rc = finish_linear(h, canon, bias, st))) { free_linear(h); return rc; }
     *out = h;
     return DLLM_OK;
 }
@@ -1725,21 +1895,8 @@ int dllm_linear_create(const float *W, const float *bias, size_t K, size_t N, ui
 int dllm_linear_create_quantized(const uint8_t *packed_codes, const float *scales, const uint8_t *zps,
                                  const float *bias, size_t K, size_t N, uint8_t bits, size_t group,
                                  dllm_linear_t *out, dllm_stream_t stream) {
-    if (!out || !packed_codes || !scales || !zps) return fail(DLLM_ERR_INVALID_PARAMS, "null pointer");
-    int rc = check_shape(K, N, bits, group);
-    if (rc) return rc;
-    dllm_linear *h = nullptr;
-    if ((rc = alloc_linear(K, N, bits, group, &h))) return rc;
-    hipStream_t st = as_stream(stream);
-    const size_t nbytes = (K * N * bits + 7) / 8;
-    hipError_t e = hipMemsetAsync(h->canon, 0, canon_words(K, N, bits) * 4, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(h->canon, packed_codes, nbytes, hipMemcpyDeviceToDevice, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(h->scales, scales, h->G * N * 4, hipMemcpyDeviceToDevice, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(h->zps, zps, h->G * N, hipMemcpyDeviceToDevice, st);
-    if (e != hipSuccess) { free_linear(h); return fail(DLLM_ERR_HIP, hipGetErrorString(e)); }
-    if ((rc = finish_linear(h, bias, st))) { free_linear(h); return rc; }
-    *out = h;
-    return DLLM_OK;
+    return dllm_linear_create_quantized_ex(packed_codes, scales, zps, bias, K, N, bits, group, DLLM_PRECISION_EXACT,
+                                           out, stream);
 }
 
 // f16 view of X: as given, or cast from f32 through the handle's workspace.
@@ -1804,8 +1961,11 @@ int dllm_linear_forward_psample(dllm_linear_t h, const void *X, size_t M, int x_
     hipStream_t st = as_stream(stream);
     const __half *Xh = nullptr;
     if (const int rc = prepare_x(h, X, M, x_dtype, st, &Xh)) return rc;
-    if (M <= static_cast<size_t>(kDecodeMaxM) ||
-        (h->variant != 4 && h->variant != 5 && h->variant < 7)) {
+    bool fused = M > static_cast<size_t>(kDecodeMaxM);
+#if DLLM_LAB
+    fused = fused && !((h->variant >= 0 && h->variant <= 3) || h->variant == 5 || h->variant == 6);
+#endif
+    if (!fused) {
         // Paths without the fused epilogue: f32 eps through a per-stream workspace, then p_sample
         // (the same eps bits, hence the same result as the fused form on that path).
         float *eps = device_workspace(st, M * h->N * sizeof(float), 1);
@@ -1839,9 +1999,12 @@ int dllm_linear_forward_psample(dllm_linear_t h, const void *X, size_t M, int x_
 int dllm_linear_export(dllm_linear_t h, uint8_t *packed_codes, float *scales, uint8_t *zps, dllm_stream_t stream) {
     if (!h) return fail(DLLM_ERR_INVALID_PARAMS, "null handle");
     hipStream_t st = as_stream(stream);
-    if (packed_codes)
-        DLLM_HIP_TRY(hipMemcpyAsync(packed_codes, h->canon, (h->K * h->N * h->bits + 7) / 8,
-                                    hipMemcpyDeviceToDevice, st));
+    if (packed_codes) {
+        const size_t nbytes = (h->K * h->N * h->bits + 7) / 8;
+        export_codes_kernel<<<grid_for(nbytes, 256, kCUs * 16), 256, 0, st>>>(h->wdev, h->K, h->N, h->bits,
+                                                                               packed_codes, nbytes);
+        DLLM_LAUNCH_CHECK();
+    }
     if (scales) DLLM_HIP_TRY(hipMemcpyAsync(scales, h->scales, h->G * h->N * 4, hipMemcpyDeviceToDevice, st));
     if (zps) DLLM_HIP_TRY(hipMemcpyAsync(zps, h->zps, h->G * h->N, hipMemcpyDeviceToDevice, st));
     return DLLM_OK;
@@ -1856,11 +2019,32 @@ int dllm_linear_info(dllm_linear_t h, size_t *K, size_t *N, uint8_t *bits, size_
     return DLLM_OK;
 }
 
-size_t dllm_linear_weight_bytes(dllm_linear_t h) {
-    if (!h) return 0;
-    return h->Npad * h->K * h->bits / 8 + h->G * h->Npad * 4;   // one layout is read per forward
+int dllm_linear_precision(dllm_linear_t h) {
+    if (!h) {
+        fail(DLLM_ERR_INVALID_PARAMS, "null handle");
+        return -1;
+    }
+    return h->precision;
 }
 
+size_t dllm_linear_weight_bytes(dllm_linear_t h) {
+    if (!h) return 0;
+    // one layout is read per forward: the packed codes + one 4-B {zp, scale} word per (group, column)
+    // (+ the 4-B f32 scale on the exact-weight path)
+    return h->Npad * h->K * h->bits / 8 + h->G * h->Npad * (use_exact(h) ? 8 : 4);
+}
+
+size_t dllm_linear_device_bytes(dllm_linear_t h) {
+    if (!h) return 0;
+    size_t b = h->Npad * h->K * h->bits / 8 + h->Npad * ((h->K + 127) / 128) * 128 * h->bits / 8   // wdev + wdec
+               + h->G * h->Npad * 8 + h->G * h->N * 5 + h->Npad * 4;                              // sz, sf, scales, zps, bias
+#if DLLM_LAB
+    b += h->Npad * h->K * h->bits / 8;
+#endif
+    return b + h->xws_elems * sizeof(__half);
+}
+
+#if DLLM_LAB
 int dllm_linear_set_kernel_variant(dllm_linear_t h, int variant) {
     if (!h) return fail(DLLM_ERR_INVALID_PARAMS, "null handle");
     if (variant >= 200 && variant < 264) {   // decode (NT, nsplit) override (measurement only)
@@ -1880,12 +2064,13 @@ int dllm_linear_set_kernel_variant(dllm_linear_t h, int variant) {
         h->pplab = (variant - 100) % 32;
         return DLLM_OK;
     }
-    if (variant < 0 || variant > 13)
-        return fail(DLLM_ERR_INVALID_PARAMS, "variant must be 0..13 (16..23, 32..95, 100..195, 200..263: ablations)");
+    if (variant < -1 || variant > 15)
+        return fail(DLLM_ERR_INVALID_PARAMS, "variant must be -1..15 (16..23, 32..95, 100..195, 200..263: ablations)");
     h->variant = variant;
     h->dlab = h->rlab = h->pplab = h->dcfg = 0;
     return DLLM_OK;
 }
+#endif
 
 int dllm_linear_destroy(dllm_linear_t h) {
     free_linear(h);

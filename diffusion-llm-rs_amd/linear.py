@@ -14,32 +14,41 @@ from ._lib import check
 from .quantization import _dev, _ptr, _stream
 
 
-class QuantLinear:
-    """Owns a ``dllm_linear_t`` handle (device weights uploaded once; immutable; Send + Sync)."""
+EXACT, F16W = 0, 1   # DLLM_PRECISION_EXACT (default), DLLM_PRECISION_F16W
 
-    def __init__(self, handle, K: int, N: int, bits: int, group: int):
+
+class QuantLinear:
+    """Owns a ``dllm_linear_t`` handle (device weights uploaded once; immutable; Send + Sync).
+
+    ``precision``: EXACT (default) feeds the MFMA the exact integer (q - zp) and applies the f32
+    scale per group, so the weight is the reference's f32 a2 value; F16W rounds the dequantized
+    weight to f16 first (faster at M >= 4096, ~2.7e-4 more relative error per layer)."""
+
+    def __init__(self, handle, K: int, N: int, bits: int, group: int, precision: int = EXACT):
         self._h = handle
-        self.K, self.N, self.bits, self.group = K, N, bits, group
+        self.K, self.N, self.bits, self.group, self.precision = K, N, bits, group, precision
 
     @classmethod
-    def from_weight(cls, W: torch.Tensor, bias: torch.Tensor | None = None, bits: int = 4, group: int = 128):
+    def from_weight(cls, W: torch.Tensor, bias: torch.Tensor | None = None, bits: int = 4, group: int = 128,
+                    precision: int = EXACT):
         """W f32 [K, N] (the reference's ``weights: Array2<f32>`` of shape [input_dim, output_dim])."""
         W = _dev(W, torch.float32)
         K, N = W.shape
         b = None if bias is None else _dev(bias, torch.float32)
         h = C.c_void_p()
-        check(_lib.load().dllm_linear_create(_ptr(W), _ptr(b), K, N, bits, group, C.byref(h), _stream()))
-        return cls(h, K, N, bits, group)
+        check(_lib.load().dllm_linear_create_ex(_ptr(W), _ptr(b), K, N, bits, group, int(precision), C.byref(h),
+                                                _stream()))
+        return cls(h, K, N, bits, group, precision)
 
     @classmethod
     def from_quantized(cls, packed_codes: torch.Tensor, scales: torch.Tensor, zps: torch.Tensor, K: int, N: int,
-                       bits: int = 4, group: int = 128, bias: torch.Tensor | None = None):
+                       bits: int = 4, group: int = 128, bias: torch.Tensor | None = None, precision: int = EXACT):
         h = C.c_void_p()
         b = None if bias is None else _dev(bias, torch.float32)
-        check(_lib.load().dllm_linear_create_quantized(
+        check(_lib.load().dllm_linear_create_quantized_ex(
             _ptr(_dev(packed_codes, torch.uint8)), _ptr(_dev(scales, torch.float32)), _ptr(_dev(zps, torch.uint8)),
-            _ptr(b), K, N, bits, group, C.byref(h), _stream()))
-        return cls(h, K, N, bits, group)
+            _ptr(b), K, N, bits, group, int(precision), C.byref(h), _stream()))
+        return cls(h, K, N, bits, group, precision)
 
     def forward(self, x: torch.Tensor, out: torch.Tensor | None = None, out_dtype=torch.float16) -> torch.Tensor:
         """``forward(x) = x . W^ + b`` for x [M, K] (f16 or f32) -> [M, N]."""
@@ -92,9 +101,16 @@ class QuantLinear:
         check(_lib.load().dllm_linear_export(self._h, _ptr(codes), _ptr(scales), _ptr(zps), _stream()))
         return codes, scales, zps
 
+    def device_bytes(self) -> int:
+        """Device memory the handle owns (dllm_linear_device_bytes)."""
+        return int(_lib.load().dllm_linear_device_bytes(self._h))
+
     def set_kernel_variant(self, variant: int):
-        """Prefill GEMM schedule variant (tuning / A-B benchmarking)."""
-        check(_lib.load().dllm_linear_set_kernel_variant(self._h, int(variant)))
+        """Schedule variant / ablation mask: lab build only (DLLM_LIB=lab, measurement scripts)."""
+        lib = _lib.load()
+        if not hasattr(lib, "dllm_linear_set_kernel_variant"):
+            raise _lib.UnsupportedOperation("schedule variants exist only in the lab build (DLLM_LIB=lab)", 2)
+        check(lib.dllm_linear_set_kernel_variant(self._h, int(variant)))
 
     def weight_bytes(self) -> int:
         return int(_lib.load().dllm_linear_weight_bytes(self._h))

@@ -15,8 +15,9 @@
  *     host pointers, stage through device memory and synchronise (parity/test convenience).
  *   - quantized codes are either one code per byte ("unpacked", the reference's storage,
  *     diffuse-llm-rs/src/quantization.rs:59-65) or the packed LSB-first bitstream below.
- *   - handles (dllm_linear_t) own device memory, are immutable after create and may be used
- *     from several threads on distinct streams (the reference's Send + Sync model bound).
+ *   - handles (dllm_linear_t) own device memory, are immutable after create (the lab build's
+ *     dllm_linear_set_kernel_variant aside) and may be used from several threads on distinct
+ *     streams (the reference's Send + Sync model bound).
  *
  * Packed layout (build-defined; the reference only assumes its size, quantization.rs:122):
  *   element i of an n-element, b-bit tensor occupies bits [i*b, (i+1)*b) of a little-endian
@@ -180,19 +181,33 @@ int dllm_decompress_vectors(const uint8_t *q, size_t rows, size_t dim, const flo
  * W [K, N] ("[input_dim, output_dim]", :776-777), with W quantized per (output column n, K-group g
  * of `group` rows) by quantize_tensor (a1, bits in {2,4,8}) and dequantized by a2 inside the
  * GEMM.  group = QuantizationConfig::default().group_size = 128 (quantization/src/types.rs:124-127).
- * Device compute: dequantized weight rounded to f16, f16 MFMA with f32 accumulation, bias in f32.
+ * Device compute: X in f16, f16 MFMA with f32 accumulation, bias in f32; the dequantized weight
+ * (q - zp) * scale of a2 reaches the MFMA in one of two precisions:
+ *   DLLM_PRECISION_EXACT (default): the MFMA operand is the exact integer (q - zp) and the f32
+ *     scale multiplies each group's f32 partial sum, so the weight is the reference's f32 a2 value;
+ *     the only operand rounding is X's (f16).  Needs group in {64, 128, 256} and K % group == 0
+ *     (other shapes use the F16W arithmetic).
+ *   DLLM_PRECISION_F16W: the weight is rounded to f16 (f16((q - zp) * f16(scale))) before the MFMA;
+ *     ~2.7e-4 more relative error per layer, and faster at M >= 4096 (256 x 256 tiles).
  * Requirements: K % 64 == 0, group % 64 == 0; any M >= 0, any N >= 1. */
 typedef struct dllm_linear *dllm_linear_t;
+enum dllm_precision { DLLM_PRECISION_EXACT = 0, DLLM_PRECISION_F16W = 1 };
 
 /* W (device, f32 [K][N] row-major), bias (device f32 [N] or NULL = zeros, the reference's
- * Array1::zeros, lib.rs:798).  Quantization runs on the GPU (bit-exact with a1). */
+ * Array1::zeros, lib.rs:798).  Quantization runs on the GPU (bit-exact with a1).  Precision
+ * DLLM_PRECISION_EXACT. */
 int dllm_linear_create(const float *W, const float *bias, size_t K, size_t N, uint8_t bits, size_t group,
                        dllm_linear_t *out, dllm_stream_t stream);
+int dllm_linear_create_ex(const float *W, const float *bias, size_t K, size_t N, uint8_t bits, size_t group,
+                          int precision, dllm_linear_t *out, dllm_stream_t stream);
 /* Import already-quantized weights: codes packed in the canonical bitstream of the [K][N]
  * row-major code matrix, scales f32 [G][N], zps u8 [G][N] (G = ceil(K/group)); all device. */
 int dllm_linear_create_quantized(const uint8_t *packed_codes, const float *scales, const uint8_t *zps,
                                  const float *bias, size_t K, size_t N, uint8_t bits, size_t group,
                                  dllm_linear_t *out, dllm_stream_t stream);
+int dllm_linear_create_quantized_ex(const uint8_t *packed_codes, const float *scales, const uint8_t *zps,
+                                    const float *bias, size_t K, size_t N, uint8_t bits, size_t group,
+                                    int precision, dllm_linear_t *out, dllm_stream_t stream);
 /* Y[M][N] = X[M][K] . W^ + b.  x_dtype/y_dtype in {DLLM_F32, DLLM_F16}; an f32 X is cast to f16
  * through a workspace owned by the handle.  Shapes with too few output tiles to fill the GPU
  * (M roughly 65..1000 at N = 4096) split K into slices whose f32 partials are combined in slice
@@ -200,19 +215,24 @@ int dllm_linear_create_quantized(const uint8_t *packed_codes, const float *scale
  * are allocated on the first call that needs them, which therefore must precede stream capture. */
 int dllm_linear_forward(dllm_linear_t h, const void *X, size_t M, int x_dtype, void *Y, int y_dtype,
                         dllm_stream_t stream);
-/* Export the quantized weights in canonical form (packed bitstream [K][N], scales [G][N], zps). */
+/* Export the quantized weights in canonical form (packed bitstream [K][N], scales [G][N], zps);
+ * the codes are rebuilt from the device layout (the handle keeps no canonical copy). */
 int dllm_linear_export(dllm_linear_t h, uint8_t *packed_codes, float *scales, uint8_t *zps,
                        dllm_stream_t stream);
 int dllm_linear_info(dllm_linear_t h, size_t *K, size_t *N, uint8_t *bits, size_t *group);
+int dllm_linear_precision(dllm_linear_t h);   /* DLLM_PRECISION_*, -1 on a null handle */
 /* HBM bytes the forward's GEMM kernel reads for the weights (packed codes + scales/zps). */
 size_t dllm_linear_weight_bytes(dllm_linear_t h);
-/* Tuning knob (benchmarks / A-B runs).  4 (default): tile policy over the 3-stage-ring kernels
- * (256x256, 256x128, 128x128 + split-K); 5: same; 0..3: the 2-stage 256x128 schedules;
- * 6: 2-stage kernels with 128-row tiles + split-K below 256 tiles; 7: 256x256 tile, 2x4 waves;
- * 8: 256x256 tile on the 16x16x32 MFMA; 9/10: ping-pong wave groups (1/2 substeps per phase);
- * 11: ping-pong on the 16x16x32 MFMA.  16..23, 32..95, 100..195: ablation masks of the decode,
- * ring and ping-pong kernels (measurement only: loads or math replaced, results are garbage). */
+/* Device memory the handle owns (two code layouts -- prefill and decode fragments -- and the
+ * per-(group, column) parameters; the X staging workspace once grown). */
+size_t dllm_linear_device_bytes(dllm_linear_t h);
+#ifdef DLLM_LAB
+/* Lab build only (libdllm_hip_lab.so): A/B schedule variants and ablation masks; mutates the
+ * handle, so it is not part of the product ABI.  -1: product policy; 4: rounded-weight policy;
+ * 14 / 15: exact-weight 128x256 / tile-major 256x256; 0..3, 5..13: round-1 schedules;
+ * 16..23, 32..95, 100..195: ablation masks (results are garbage); 200..263: decode tile override. */
 int dllm_linear_set_kernel_variant(dllm_linear_t h, int variant);
+#endif
 int dllm_linear_destroy(dllm_linear_t h);
 
 /* ---- a9: int-quantized KV dequant-attention (consumer of QuantizedKVCacheEntry) -------------

@@ -1,9 +1,14 @@
 """Per-launch HBM traffic of the bench GEMM kernel from rocprofv3 PMC passes (MI355X_MICROARCH.md
-HBM section: FETCH_SIZE reads 1/2 of a wide coalesced stream on gfx950 -> doubled; WRITE_SIZE is
-exact for 16-B stores; both in KiB).  Writes profiles/<tag>_pmc_gemm.json."""
+HBM section: FETCH_SIZE reads 1/2 of a wide coalesced stream on gfx950 -> doubled, a factor this
+repo re-checks with scripts/pmc_calib.py; WRITE_SIZE is exact for 16-B stores; both in KiB).
+Usage: pmc_to_json.py <pmc root> <out.json> <kernel substring> [M K N_local bits group]; the config
+is recorded so bench.py only quotes the figure for the same shape."""
 import csv, glob, json, statistics, sys
 root, out = sys.argv[1], sys.argv[2]
 regex = sys.argv[3] if len(sys.argv) > 3 else "wq_gemm8_kernel<4,"
+cfg = None
+if len(sys.argv) > 8:
+    cfg = dict(zip(("M", "K", "N_local", "bits", "group"), (int(v) for v in sys.argv[4:9])))
 vals = {}
 for f in glob.glob(f"{root}/**/pmc_counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
@@ -15,6 +20,8 @@ res = {"kernel": regex, "FETCH_SIZE_bytes_raw": fetch, "WRITE_SIZE_bytes": write
        "hbm_bytes_per_launch": 2 * fetch + write,
        "correction": "FETCH_SIZE doubled (gfx950 reports 1/2 of wide coalesced reads); Infinity-Cache hits are counted",
        "dispatches": len(vals["FETCH_SIZE"])}
+if cfg is not None:
+    res["config"] = cfg
 for k, v in vals.items():
     if k not in ("FETCH_SIZE", "WRITE_SIZE"):
         res[k] = statistics.median(v)

@@ -10,6 +10,17 @@ if str(ROOT) not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU; run with -m gpu")
+    config.addinivalue_line("markers", "lab: A/B schedules of the lab build (DLLM_LIB=lab); skipped otherwise")
+
+
+def pytest_collection_modifyitems(config, items):
+    import os
+    if os.environ.get("DLLM_LIB") == "lab":
+        return
+    skip = pytest.mark.skip(reason="lab-build schedule (set DLLM_LIB=lab with lib/libdllm_hip_lab.so built)")
+    for it in items:
+        if "lab" in it.keywords:
+            it.add_marker(skip)
 
 
 @pytest.fixture(scope="session")

@@ -11,8 +11,10 @@ ROOT = Path(__file__).resolve().parents[1]
 HEADER = ROOT / "include" / "dllm_quant.h"
 
 
-def declared_symbols():
+def declared_symbols(lab=False):
     text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    if not lab:   # the lab build's entry points are not part of the product ABI
+        text = re.sub(r"#ifdef DLLM_LAB.*?#endif", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(dllm_\w+)\s*\(", text)))
 
 
@@ -23,6 +25,10 @@ def test_header_symbols_exported(dllm):
     for s in syms:
         assert hasattr(lib, s), f"{s} declared in dllm_quant.h but not exported"
     assert set(syms) == set(dllm._lib.SIGNATURES), "ctypes signature table out of sync with the header"
+    lab_only = set(declared_symbols(lab=True)) - set(syms)
+    assert lab_only == set(dllm._lib.LAB_SIGNATURES)
+    for s in lab_only:   # the product library carries no A/B knobs
+        assert not hasattr(lib, s), f"{s} is lab-only but the product library exports it"
 
 
 def test_library_is_gfx950(dllm):
