@@ -57,6 +57,23 @@ __device__ __forceinline__ void glds4_asm(const void *gsrc, uint32_t lds_dst) {
                  : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
 }
 
+// LDS-DMA through a buffer descriptor: address = base(rs) + voff (per lane, fixed) + soff (wave-
+// uniform, advances per stage), so a stage's DMAs need no per-lane address arithmetic.
+__device__ __forceinline__ void blds16_asm(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff, uint32_t lds_dst) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(rs), "s"(lds_dst), "s"(soff) : "memory");
+}
+__device__ __forceinline__ void blds4_asm(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff, uint32_t lds_dst) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(rs), "s"(lds_dst), "s"(soff) : "memory");
+}
+// Raw buffer descriptor over [base, base + 4 GiB) (no range clamp is relied on).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t raw_rsrc(const void *base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, 0x7FFFFFFF, 0x00020000);
+}
+
 constexpr int kWave = 64;      // CDNA wavefront width
 constexpr int kCUs = 256;      // MI355X compute units (8 XCDs x 32)
 constexpr int kXCDs = 8;

@@ -73,7 +73,13 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
     const int xcd = orig % kXCDs, q8 = nb / kXCDs, r8 = nb % kXCDs;
     const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / kXCDs;
     const int ks = wgid / (nbm * nbn), tile = wgid % (nbm * nbn);
-    const int bm = tile / nbn, bn = tile % nbn;
+    // Tiles in groups of 4 row-blocks, column-major inside a group: the 32 blocks an XCD runs at
+    // once cover 4 row-blocks x 8 column-blocks, so a 64-deep slab costs that XCD's L2 4 X tiles +
+    // 8 weight tiles of fetch (row-major order: 2 + 16, 25 % more).
+    constexpr int kGM = 4;
+    const int grp = tile / (kGM * nbn), first = grp * kGM, gm = min(kGM, nbm - first);
+    const int in_grp = tile - grp * kGM * nbn;
+    const int bm = first + in_grp % gm, bn = in_grp / gm;
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -84,21 +90,25 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
     const unsigned spg = static_cast<unsigned>(group) / kBK;                // slabs per group
     const unsigned nt = static_cast<unsigned>(n0 + wave * 32) >> 5;
 
+    // DMA sources as buffer descriptors (wave-uniform bases) + fixed per-lane offsets; a stage only
+    // moves the scalar offset.  X: the block's first row; rows past M are clamped to M - 1.
     const int chunk_st = lane & 7;
-    const __half *xsrc[SL::kR1];
+    uint32_t xoff[SL::kR1];
 #pragma unroll
     for (int i = 0; i < SL::kR1; ++i) {
         const int row = (i * NW + wave) * 8 + (lane >> 3);
-        int grow = m0 + row;
-        grow = grow < M ? grow : M - 1;
+        const int rrow = (m0 + row < M ? m0 + row : M - 1) - m0;
         const int c = chunk_st ^ ((row >> 1) & 7);
-        xsrc[i] = X + static_cast<size_t>(grow) * K + c * 8;
+        xoff[i] = static_cast<uint32_t>((rrow * K + c * 8) * 2);
     }
-    const uint32_t *wsrc = wdev + (static_cast<size_t>(nt) * nk_all * 64 + lane) * BITS;
+    const __amdgpu_buffer_rsrc_t xrs = raw_rsrc(X + static_cast<size_t>(m0) * K);
+    const __amdgpu_buffer_rsrc_t wrs = raw_rsrc(wdev + static_cast<size_t>(nt) * nk_all * 64 * BITS);
+    const uint32_t woff = static_cast<uint32_t>(lane * BITS * 4);
     const int ncol = lane & (8 * NW - 1);                    // 4 columns per lane (NW = 4: lanes 32.. mirror)
-    const uint32_t *szsrc = sz + n0 + 4 * ncol;
-    const float *sfsrc = sf + n0 + 4 * ncol;
     const bool has_sz = wave == 0, has_sf = wave == 1;
+    // wave 0 stages the zero-point pairs, wave 1 the f32 scales: the same byte offsets in two arrays
+    const __amdgpu_buffer_rsrc_t prs = raw_rsrc(has_sz ? static_cast<const void *>(sz + n0) : static_cast<const void *>(sf + n0));
+    const uint32_t poff = static_cast<uint32_t>(16 * ncol);
     const uint32_t wv = static_cast<uint32_t>(wave);
 
     // LDS destinations go through readfirstlane: the M0 operand must be an SGPR, and hipcc's
@@ -111,24 +121,24 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
         for (int s = 0; s < SPS; ++s)
 #pragma unroll
             for (int i = 0; i < SL::kR1; ++i)
-                glds16_asm(xsrc[i] + (slab0 + s) * kBK, u(base + s * SL::kX1 + wv * 1024 + i * NW * 1024));
+                blds16_asm(xrs, xoff[i], u((slab0 + s) * kBK * 2), u(base + s * SL::kX1 + wv * 1024 + i * NW * 1024));
 #pragma unroll
         for (int s = 0; s < SPS; ++s) {
-            const uint32_t *wp = wsrc + static_cast<size_t>(slab0 + s) * 64 * BITS;
+            const uint32_t so = u((slab0 + s) * 64 * BITS * 4);
             const uint32_t wb = u(base + SL::kX + s * SL::kW1 + wv * (64 * BITS * 4));
             if constexpr (BITS == 4) {
-                glds16_asm(wp, wb);
+                blds16_asm(wrs, woff, so, wb);
             } else if constexpr (BITS == 8) {
-                glds16_asm(wp, wb);
-                glds16_asm(wp + 4, u(wb + 64 * 16));
+                blds16_asm(wrs, woff, so, wb);
+                blds16_asm(wrs, woff + 16, so, u(wb + 64 * 16));
             } else {
-                glds4_asm(wp, wb);
-                glds4_asm(wp + 1, u(wb + 256));
+                blds4_asm(wrs, lane * 8, so, wb);
+                blds4_asm(wrs, lane * 8 + 4, so, u(wb + 256));
             }
         }
-        const size_t goff = static_cast<size_t>(slab0 / spg) * Npad;
-        if (has_sz) glds16_asm(szsrc + goff, u(base + SL::kX + SL::kW));
-        if (has_sf) glds16_asm(sfsrc + goff, u(base + SL::kX + SL::kW + SL::kSZ));
+        const uint32_t goff = u((slab0 / spg) * static_cast<uint32_t>(Npad) * 4);
+        if (has_sz) blds16_asm(prs, poff, goff, u(base + SL::kX + SL::kW));
+        if (has_sf) blds16_asm(prs, poff, goff, u(base + SL::kX + SL::kW + SL::kSZ));
     };
     // Counted wait leaving the newest stage's DMAs (this wave's own count) in flight.
     auto wait_prev = [&]() __attribute__((always_inline)) {
@@ -172,6 +182,24 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
         half8_t bA[MR], bB[MR];
         read_b(bA, sb, 0);
         half8_t aA = dequant_exact<BITS>(w[0], 0, ec), aB;
+        // Scales of this group (lane half hsel holds columns 4 hsel + 8 qd + (0..3) of the wave's 32),
+        // read at the head of the stage so the fold never waits on LDS.
+        float4 s4[4];
+        if constexpr (GL) {
+            const float *sfl = reinterpret_cast<const float *>(sb + SL::kX + SL::kW + SL::kSZ) + wave * 32 + 4 * hsel;
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd) s4[qd] = *reinterpret_cast<const float4 *>(sfl + 8 * qd);
+        }
+        // acc[r] += s (.) T_g[r]
+        auto fold = [&](int r) __attribute__((always_inline)) {
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd) {
+                acc[r][4 * qd + 0] = __builtin_fmaf(s4[qd].x, tacc[r][4 * qd + 0], acc[r][4 * qd + 0]);
+                acc[r][4 * qd + 1] = __builtin_fmaf(s4[qd].y, tacc[r][4 * qd + 1], acc[r][4 * qd + 1]);
+                acc[r][4 * qd + 2] = __builtin_fmaf(s4[qd].z, tacc[r][4 * qd + 2], acc[r][4 * qd + 2]);
+                acc[r][4 * qd + 3] = __builtin_fmaf(s4[qd].w, tacc[r][4 * qd + 3], acc[r][4 * qd + 3]);
+            }
+        };
         auto sub = [&](half8_t (&bc)[MR], half8_t (&bn)[MR], const half8_t &ac, half8_t &an, auto v_tag) __attribute__((always_inline)) {
             constexpr int v = decltype(v_tag)::value;
             __builtin_amdgcn_sched_barrier(0);
@@ -179,15 +207,31 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
             if constexpr (v + 1 < kSub) {
                 read_b(bn, sb, v + 1);
                 an = dequant_exact<BITS>(w[(v + 1) / 4], (v + 1) % 4, ec);
-            }
 #pragma unroll
-            for (int r = 0; r < MR; ++r)
-                tacc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bc[r], (GF && v == 0) ? zero16 : tacc[r], 0, 0, 0);
+                for (int r = 0; r < MR; ++r)
+                    tacc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bc[r], (GF && v == 0) ? zero16 : tacc[r], 0, 0, 0);
 #pragma unroll
-            for (int i = 0; i < MR; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
-                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);   // VALU
+                for (int i = 0; i < MR; ++i) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+                    __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);   // VALU
+                }
+            } else {
+                // Last substep: rep r's fold follows rep r+1's MFMA, so the fold of a group runs
+                // beside the group's own last MFMAs instead of after all of them.
+#pragma unroll
+                for (int r = 0; r < MR; ++r)
+                    tacc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bc[r], (GF && v == 0) ? zero16 : tacc[r], 0, 0, 0);
+                if constexpr (GL) {
+#pragma unroll
+                    for (int r = 0; r < MR; ++r) fold(r);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // MFMA r = 0, 1
+#pragma unroll
+                    for (int i = 2; i < MR; ++i) {
+                        __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);  // fold of rep i - 2
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA rep i
+                    }
+                }
             }
             __builtin_amdgcn_s_setprio(0);
             __builtin_amdgcn_sched_barrier(0);
@@ -196,22 +240,6 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
             ((Vs % 2 == 0 ? sub(bA, bB, aA, aB, std::integral_constant<int, Vs>{})
                           : sub(bB, bA, aB, aA, std::integral_constant<int, Vs>{})), ...);
         }(std::make_integer_sequence<int, kSub>{});
-        if constexpr (GL) {
-            // acc += s (.) T_g: lane half hsel holds columns 4 hsel + 8 qd + (0..3) of the wave's 32.
-            const float *sfl = reinterpret_cast<const float *>(sb + SL::kX + SL::kW + SL::kSZ) + wave * 32 + 4 * hsel;
-            float4 s4[4];
-#pragma unroll
-            for (int qd = 0; qd < 4; ++qd) s4[qd] = *reinterpret_cast<const float4 *>(sfl + 8 * qd);
-#pragma unroll
-            for (int r = 0; r < MR; ++r)
-#pragma unroll
-                for (int qd = 0; qd < 4; ++qd) {
-                    acc[r][4 * qd + 0] = __builtin_fmaf(s4[qd].x, tacc[r][4 * qd + 0], acc[r][4 * qd + 0]);
-                    acc[r][4 * qd + 1] = __builtin_fmaf(s4[qd].y, tacc[r][4 * qd + 1], acc[r][4 * qd + 1]);
-                    acc[r][4 * qd + 2] = __builtin_fmaf(s4[qd].z, tacc[r][4 * qd + 2], acc[r][4 * qd + 2]);
-                    acc[r][4 * qd + 3] = __builtin_fmaf(s4[qd].w, tacc[r][4 * qd + 3], acc[r][4 * qd + 3]);
-                }
-        }
         // Stage kt+1 must have landed; kt+2's DMAs may stay in flight across the barrier.
         if (issue) wait_prev();
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
