@@ -128,6 +128,18 @@ SIGNATURES = {
     "dllm_bit_dequantize_host": (INT, [P, S, FL, FL, P]),
     "dllm_compress_vector_host": (INT, [P, S, U8, P, P, P]),
     "dllm_linear_create_host": (INT, [P, P, S, S, U8, S, P]),
+    "dllm_format_f32": (INT, [FL, P, S, P]),
+    "dllm_qparams_to_bincode": (INT, [P, P, S, P]),
+    "dllm_qparams_from_bincode": (INT, [P, S, INT, P, P]),
+    "dllm_qparams_to_json": (INT, [P, P, S, P]),
+    "dllm_qparams_from_json": (INT, [P, S, P]),
+    "dllm_qtensor_to_bincode": (INT, [P, S, P, S, P, P, S, P]),
+    "dllm_qtensor_from_bincode": (INT, [P, S, INT, P, S, P, P, S, P, P]),
+    "dllm_qtensor_to_json": (INT, [P, S, P, S, P, P, S, P]),
+    "dllm_qtensor_from_json": (INT, [P, S, P, S, P, P, S, P, P]),
+    "dllm_compressed_vector_to_bincode": (INT, [P, S, P, S, U8, P, S, FL, FL, P, S, P]),
+    "dllm_compressed_vector_from_bincode": (INT, [P, S, INT, P, S, P, P, S, P, P, P, S, P, P, P]),
+    "dllm_compressed_vector_to_json": (INT, [P, S, P, S, U8, P, S, FL, FL, P, S, P]),
     "dllm_linear_forward_host": (INT, [P, P, S, P]),
 }
 

@@ -235,6 +235,48 @@ int dllm_linear_set_kernel_variant(dllm_linear_t h, int variant);
 #endif
 int dllm_linear_destroy(dllm_linear_t h);
 
+/* ---- f3: wire formats (host buffers; no device work) --------------------------------------
+ * The serde derives of QuantizationParams / QuantizedTensor (quantization/src/types.rs:19-47) and
+ * CompressedVector (diffusion_prefill/src/prefill_kv.rs:25-33) in the two encodings the reference's
+ * crates use (bincode 1.3 legacy, quantization/src/error.rs:44-47; serde_json, :48-53):
+ * bincode = little-endian fixed-width, usize as u64, Vec/String = u64 length + items, bool 1 byte,
+ * Option = 1-byte tag (+ value); json = compact serde_json, f32 as ryu's shortest digits, non-finite
+ * as null.  Encoders write into out[cap] and always set *len to the size needed (out = NULL: size
+ * query; cap too small: DLLM_ERR_SERIALIZATION).  Decoders: strict = 0 ignores trailing bytes like
+ * bincode::deserialize, strict = 1 rejects them; output arrays may be NULL to query their counts;
+ * malformed input -> DLLM_ERR_SERIALIZATION (QuantizationError::Serialization). */
+typedef struct dllm_qparams {
+    uint8_t bits;
+    float scale;
+    int32_t zero_point;
+    uint8_t symmetric;
+    uint8_t has_axis;   /* Option<usize> axis */
+    uint64_t axis;
+} dllm_qparams;
+int dllm_format_f32(float x, char *out, size_t cap, size_t *len);   /* serde_json's f32 text */
+int dllm_qparams_to_bincode(const dllm_qparams *p, uint8_t *out, size_t cap, size_t *len);
+int dllm_qparams_from_bincode(const uint8_t *buf, size_t len, int strict, dllm_qparams *p, size_t *consumed);
+int dllm_qparams_to_json(const dllm_qparams *p, char *out, size_t cap, size_t *len);
+int dllm_qparams_from_json(const char *s, size_t len, dllm_qparams *p);
+int dllm_qtensor_to_bincode(const uint8_t *codes, size_t n, const uint64_t *shape, size_t ndim, const dllm_qparams *p,
+                            uint8_t *out, size_t cap, size_t *len);
+int dllm_qtensor_from_bincode(const uint8_t *buf, size_t len, int strict, uint8_t *codes, size_t codes_cap, size_t *n,
+                              uint64_t *shape, size_t shape_cap, size_t *ndim, dllm_qparams *p);
+int dllm_qtensor_to_json(const uint8_t *codes, size_t n, const uint64_t *shape, size_t ndim, const dllm_qparams *p,
+                         char *out, size_t cap, size_t *len);
+int dllm_qtensor_from_json(const char *s, size_t len, uint8_t *codes, size_t codes_cap, size_t *n, uint64_t *shape,
+                           size_t shape_cap, size_t *ndim, dllm_qparams *p);
+int dllm_compressed_vector_to_bincode(const char *id, size_t id_len, const uint8_t *data, size_t n, uint8_t bits,
+                                      const uint64_t *shape, size_t ndim, float scale, float zero_point,
+                                      uint8_t *out, size_t cap, size_t *len);
+int dllm_compressed_vector_from_bincode(const uint8_t *buf, size_t len, int strict, char *id, size_t id_cap,
+                                        size_t *id_len, uint8_t *data, size_t data_cap, size_t *n, uint8_t *bits,
+                                        uint64_t *shape, size_t shape_cap, size_t *ndim, float *scale,
+                                        float *zero_point);
+int dllm_compressed_vector_to_json(const char *id, size_t id_len, const uint8_t *data, size_t n, uint8_t bits,
+                                   const uint64_t *shape, size_t ndim, float scale, float zero_point, char *out,
+                                   size_t cap, size_t *len);
+
 /* ---- a9: int-quantized KV dequant-attention (consumer of QuantizedKVCacheEntry) -------------
  * The reference dequantizes K/V (QuantizedKVCacheEntry::dequantize_keys/values,
  * diffuse-llm-rs/src/quantization.rs:160-175) and hands them to DiffusionModel::forward_with_cache
