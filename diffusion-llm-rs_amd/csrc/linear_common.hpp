@@ -135,7 +135,7 @@ __device__ __forceinline__ ExactConsts exact_consts(half2_t nz1024) {
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
         uint32_t m = mags[i];
-        asm volatile("" : "+v"(m));   // a register operand: v_and_or_b32 takes no literal on gfx950
+        asm("" : "+v"(m));   // a register operand (v_and_or_b32 takes no literal on gfx950); pure: hoisted
         c.magic[i] = m;
         const _Float16 d = static_cast<_Float16>(1024 - (1024 >> (2 * i)));   // 1024 - mag, exact
         c.nz[i] = nz1024 + half2_t{d, d};                                     // -(mag + zp), exact
