@@ -38,11 +38,9 @@ struct dllm_linear {
     int device = 0;
     int precision = DLLM_PRECISION_EXACT;
     uint32_t *wdev = nullptr;     // prefill layout (32x32x16 fragments)
-    uint32_t *wdec = nullptr;     // decode layout (16x16x32 fragments)
+    uint32_t *wdec = nullptr;     // decode layout (16x16x32 fragments), built by the first M <= 64 call
     uint32_t *sz = nullptr;       // [G][Npad] f16 pairs {-(1024 + zp), f16(scale)}
-    float *sf = nullptr;          // [G][Npad] f32 scales (exact-weight kernels), 0 in the padding
-    float *scales = nullptr;      // [G][N]
-    uint8_t *zps = nullptr;       // [G][N]
+    float *sf = nullptr;          // [G][Npad] f32 scales (exact-weight kernels; export), 0 in the padding
     float *bias = nullptr;        // [Npad]
     __half *xws = nullptr;        // f32 -> f16 staging for X
     size_t xws_elems = 0;
@@ -234,13 +232,25 @@ __global__ void __launch_bounds__(256) build_fragments16_kernel(const uint32_t *
 
 #endif  // DLLM_LAB
 
-// Canonical -> decode layout.  One thread per (column n < Npad, 128-deep slab).
-__global__ void __launch_bounds__(256) build_decode_kernel(const uint32_t *__restrict__ canon, size_t K, size_t N,
-                                                           size_t Npad, int bits, uint32_t *__restrict__ wdec) {
+// Code (k, n) from the fragment-major (prefill) layout: lane (n & 31) + 32 ((k % 16) / 8) of the
+// (n / 32, k / 64) slab, pair P = 4 ((k % 64) / 16) + (k % 8) / 2, bit bits (P % (16/bits)) + 16 (k & 1).
+__device__ __forceinline__ uint32_t wdev_code(const uint32_t *__restrict__ wdev, size_t k, size_t n, size_t nk,
+                                              int bits) {
+    const size_t ppw = 16 / bits, kk = k % 64, lane = (n & 31) + 32 * ((kk % 16) / 8);
+    const size_t P = 4 * (kk / 16) + (kk % 8) / 2;
+    const uint32_t word = wdev[(((n >> 5) * nk + k / 64) * 64 + lane) * bits + P / ppw];
+    return (word >> (bits * (P % ppw) + 16 * (k & 1))) & ((1u << bits) - 1u);
+}
+
+// Prefill layout -> decode layout, the second weight layout, built lazily by the first decode-shaped
+// call.  Word w of lane (n & 15) + 16 o in the (n / 16, 128-deep slab) tile holds 16/bits code pairs
+// (k, k + 1), k = slab 128 + 32 (P / 4) + 8 o + 2 (P % 4).  One thread per (column n < Npad, slab).
+__global__ void __launch_bounds__(256) build_decode_from_wdev_kernel(const uint32_t *__restrict__ wdev, size_t K,
+                                                                     size_t Npad, int bits, uint32_t *__restrict__ wdec) {
     const size_t n = blockIdx.x * static_cast<size_t>(256) + threadIdx.x;
     const size_t slab = blockIdx.y;
     if (n >= Npad) return;
-    const size_t nslab = (K + 127) / 128, nt = n >> 4;
+    const size_t nk = K / 64, nslab = (K + 127) / 128, nt = n >> 4;
     const int pairs_per_word = 16 / bits;
     for (int o = 0; o < 4; ++o) {
         const size_t lane = (n & 15) + 16 * o;
@@ -251,11 +261,26 @@ __global__ void __launch_bounds__(256) build_decode_kernel(const uint32_t *__res
                 const int P = w * pairs_per_word + p, t = P >> 2, v = P & 3;
                 const size_t k = slab * 128 + t * 32 + 8 * o + 2 * v;
                 uint32_t lo = 0, hi = 0;
-                if (n < N && k < K) { lo = canon_code(canon, k, n, N, bits); hi = canon_code(canon, k + 1, n, N, bits); }
+                if (k < K) { lo = wdev_code(wdev, k, n, nk, bits); hi = wdev_code(wdev, k + 1, n, nk, bits); }
                 word |= (lo << (bits * p)) | (hi << (16 + bits * p));
             }
             dst[w] = word;
         }
+    }
+}
+
+// Export of the per-(group, column) parameters from the device copies: scale = sf (f32, exact),
+// zp = -(1024 + zp) of the sz pair's low half (exact in f16).
+__global__ void __launch_bounds__(256) export_params_kernel(const float *__restrict__ sf, const uint32_t *__restrict__ sz,
+                                                            size_t G, size_t N, size_t Npad, float *__restrict__ scales,
+                                                            uint8_t *__restrict__ zps) {
+    const size_t n = blockIdx.x * static_cast<size_t>(256) + threadIdx.x;
+    const size_t g = blockIdx.y;
+    if (n >= N) return;
+    if (scales) scales[g * N + n] = sf[g * Npad + n];
+    if (zps) {
+        const _Float16 nz = __builtin_bit_cast(_Float16, static_cast<uint16_t>(sz[g * Npad + n] & 0xFFFFu));
+        zps[g * N + n] = static_cast<uint8_t>(-static_cast<float>(nz) - 1024.0f);
     }
 }
 
@@ -265,20 +290,14 @@ __global__ void __launch_bounds__(256) build_decode_kernel(const uint32_t *__res
 // bits (P % (16/bits)) + 16 (k & 1).  Inverse of build_fragments_kernel (export round trip test).
 __global__ void __launch_bounds__(256) export_codes_kernel(const uint32_t *__restrict__ wdev, size_t K, size_t N,
                                                            int bits, uint8_t *__restrict__ out, size_t nbytes) {
-    const size_t nk = K / 64, ppw = 16 / bits, per_byte = 8 / bits;
-    const uint32_t mask = (1u << bits) - 1u;
+    const size_t nk = K / 64, per_byte = 8 / bits;
     for (size_t B = blockIdx.x * static_cast<size_t>(256) + threadIdx.x; B < nbytes;
          B += static_cast<size_t>(gridDim.x) * 256) {
         uint32_t byte = 0;
         for (size_t e = 0; e < per_byte; ++e) {
             const size_t i = B * per_byte + e;
             if (i >= K * N) break;
-            const size_t k = i / N, n = i % N;
-            const size_t kk = k % 64, lane = (n & 31) + 32 * ((kk % 16) / 8);
-            const size_t P = 4 * (kk / 16) + (kk % 8) / 2;
-            const uint32_t word = wdev[(((n >> 5) * nk + k / 64) * 64 + lane) * bits + P / ppw];
-            const uint32_t code = (word >> (bits * (P % ppw) + 16 * (k & 1))) & mask;
-            byte |= code << (bits * e);
+            byte |= wdev_code(wdev, i / N, i % N, nk, bits) << (bits * e);
         }
         out[B] = static_cast<uint8_t>(byte);
     }
@@ -1544,8 +1563,28 @@ int launch_decode_lab(const dllm_linear *h, const __half *X, size_t M, YT *Y, hi
 }
 #endif
 
+// The decode layout is built on the first decode-shaped call (prefill-only layers never hold it);
+// that call must precede stream capture, like the workspaces.
+int ensure_decode_layout(const dllm_linear *hc, hipStream_t st) {
+    dllm_linear *h = const_cast<dllm_linear *>(hc);
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (h->wdec) return DLLM_OK;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(st, &cs);
+    if (cs != hipStreamCaptureStatusNone)
+        return fail(DLLM_ERR_INVALID_PARAMS, "the decode layout is built by the first M <= 64 call: run one before stream capture");
+    uint32_t *w = nullptr;
+    DLLM_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&w), h->Npad * ((h->K + 127) / 128) * 128 * h->bits / 8));
+    dim3 gd(static_cast<unsigned>((h->Npad + 255) / 256), static_cast<unsigned>((h->K + 127) / 128));
+    build_decode_from_wdev_kernel<<<gd, 256, 0, st>>>(h->wdev, h->K, h->Npad, h->bits, w);
+    if (hipGetLastError() != hipSuccess) { (void)hipFree(w); return fail(DLLM_ERR_HIP, "decode layout build launch"); }
+    h->wdec = w;
+    return DLLM_OK;
+}
+
 template <int BITS, typename YT>
 int launch_decode(const dllm_linear *h, const __half *X, size_t M, YT *Y, hipStream_t st) {
+    if (const int rc = ensure_decode_layout(h, st)) return rc;
     int nt, nsplit;
     decode_policy(static_cast<int>(M), nt, nsplit);
 #if DLLM_LAB
@@ -1759,7 +1798,7 @@ int launch_gemm(const dllm_linear *h, const __half *X, size_t M, void *Y, int y_
 void free_linear(dllm_linear *h) {
     if (!h) return;
     (void)hipFree(h->wdev); (void)hipFree(h->wdec); (void)hipFree(h->sz); (void)hipFree(h->sf);
-    (void)hipFree(h->scales); (void)hipFree(h->zps); (void)hipFree(h->bias); (void)hipFree(h->xws);
+    (void)hipFree(h->bias); (void)hipFree(h->xws);
 #if DLLM_LAB
     (void)hipFree(h->w16);
 #endif
@@ -1788,11 +1827,8 @@ int alloc_linear(size_t K, size_t N, uint8_t bits, size_t group, int precision, 
     auto A = [&](void **p, size_t bytes) { return hipMalloc(p, std::max<size_t>(bytes, 16)); };
     hipError_t e = hipSuccess;
     if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->wdev), h->Npad * K * bits / 8);
-    if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->wdec), h->Npad * ((K + 127) / 128) * 128 * bits / 8);
     if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->sz), h->G * h->Npad * 4);
     if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->sf), h->G * h->Npad * 4);
-    if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->scales), h->G * N * 4);
-    if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->zps), h->G * N);
     if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->bias), h->Npad * 4);
 #if DLLM_LAB
     if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->w16), h->Npad * K * bits / 8);
@@ -1806,8 +1842,9 @@ int alloc_linear(size_t K, size_t N, uint8_t bits, size_t group, int precision, 
 }
 
 // Device layouts from the canonical codes (`canon`, u32-addressable, ceil(K N bits / 32) words)
-// and the scales / zero points already in the handle.  `canon` is only read by these launches.
-int finish_linear(dllm_linear *h, const uint32_t *canon, const float *bias, hipStream_t st) {
+// and the scales / zero points [G][N] (all three only read by these launches).
+int finish_linear(dllm_linear *h, const uint32_t *canon, const float *scales, const uint8_t *zps, const float *bias,
+                  hipStream_t st) {
     DLLM_HIP_TRY(hipMemsetAsync(h->bias, 0, h->Npad * 4, st));
     if (bias) DLLM_HIP_TRY(hipMemcpyAsync(h->bias, bias, h->N * 4, hipMemcpyDeviceToDevice, st));
     dim3 gf(static_cast<unsigned>((h->Npad + 255) / 256), static_cast<unsigned>(h->K / 64));
@@ -1817,13 +1854,10 @@ int finish_linear(dllm_linear *h, const uint32_t *canon, const float *bias, hipS
     build_fragments16_kernel<<<gf, 256, 0, st>>>(canon, h->K, h->N, h->Npad, h->bits, h->w16);
     DLLM_LAUNCH_CHECK();
 #endif
-    dim3 gd(static_cast<unsigned>((h->Npad + 255) / 256), static_cast<unsigned>((h->K + 127) / 128));
-    build_decode_kernel<<<gd, 256, 0, st>>>(canon, h->K, h->N, h->Npad, h->bits, h->wdec);
-    DLLM_LAUNCH_CHECK();
     dim3 gs(static_cast<unsigned>((h->Npad + 255) / 256), static_cast<unsigned>(h->G));
-    build_sz_kernel<<<gs, 256, 0, st>>>(h->scales, h->zps, h->G, h->N, h->Npad, h->sz);
+    build_sz_kernel<<<gs, 256, 0, st>>>(scales, zps, h->G, h->N, h->Npad, h->sz);
     DLLM_LAUNCH_CHECK();
-    build_sf_kernel<<<gs, 256, 0, st>>>(h->scales, h->G, h->N, h->Npad, h->sf);
+    build_sf_kernel<<<gs, 256, 0, st>>>(scales, h->G, h->N, h->Npad, h->sf);
     DLLM_LAUNCH_CHECK();
     return DLLM_OK;
 }
@@ -1847,19 +1881,21 @@ int dllm_linear_create_ex(const float *W, const float *bias, size_t K, size_t N,
     // create on this stream, in stream order), not handle memory.
     const size_t cbytes = canon_words(K, N, bits) * 4;
     uint32_t *canon = reinterpret_cast<uint32_t *>(device_workspace(st, cbytes, 3));
-    if (!canon) { free_linear(h); return DLLM_ERR_HIP; }
+    float *scales = device_workspace(st, h->G * N * 4 + h->G * N, 4);   // scales [G][N] f32, then zps u8
+    if (!canon || !scales) { free_linear(h); return DLLM_ERR_HIP; }
+    uint8_t *zps = reinterpret_cast<uint8_t *>(scales + h->G * N);
     hipError_t e = hipMemsetAsync(canon, 0, cbytes, st);
     if (e != hipSuccess) { free_linear(h); return fail(DLLM_ERR_HIP, hipGetErrorString(e)); }
     if (N % 4 == 0 && group <= 128 && (bits == 2 || bits == 4 || bits == 8) &&
         (reinterpret_cast<uintptr_t>(W) & 15) == 0) {
         dim3 g(static_cast<unsigned>((N + 255) / 256), static_cast<unsigned>(h->G));
-        quantize_weights4_kernel<<<g, 256, 0, st>>>(W, K, N, bits, static_cast<int>(group), canon, h->scales, h->zps);
+        quantize_weights4_kernel<<<g, 256, 0, st>>>(W, K, N, bits, static_cast<int>(group), canon, scales, zps);
     } else {
         dim3 g(static_cast<unsigned>((N + 255) / 256), static_cast<unsigned>(h->G));
-        quantize_weights_kernel<<<g, 256, 0, st>>>(W, K, N, bits, static_cast<int>(group), canon, h->scales, h->zps);
+        quantize_weights_kernel<<<g, 256, 0, st>>>(W, K, N, bits, static_cast<int>(group), canon, scales, zps);
     }
     if (hipGetLastError() != hipSuccess) { free_linear(h); return fail(DLLM_ERR_HIP, "quantize_weights launch"); }
-    if ((rc = finish_linear(h, canon, bias, st))) { free_linear(h); return rc; }
+    if ((rc = finish_linear(h, canon, scales, zps, bias, st))) { free_linear(h); return rc; }
     *out = h;
     return DLLM_OK;
 }
@@ -1884,10 +1920,8 @@ int dllm_linear_create_quantized_ex(const uint8_t *packed_codes, const float *sc
     if (!canon) { free_linear(h); return DLLM_ERR_HIP; }
     hipError_t e = hipMemsetAsync(canon, 0, cbytes, st);
     if (e == hipSuccess) e = hipMemcpyAsync(canon, packed_codes, nbytes, hipMemcpyDeviceToDevice, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(h->scales, scales, h->G * N * 4, hipMemcpyDeviceToDevice, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(h->zps, zps, h->G * N, hipMemcpyDeviceToDevice, st);
     if (e != hipSuccess) { free_linear(h); return fail(DLLM_ERR_HIP, hipGetErrorString(e)); }
-    if ((rc = finish_linear(h, canon, bias, st))) { free_linear(h); return rc; }
+    if ((rc = finish_linear(h, canon, scales, zps, bias, st))) { free_linear(h); return rc; }
     *out = h;
     return DLLM_OK;
 }
@@ -2005,8 +2039,11 @@ int dllm_linear_export(dllm_linear_t h, uint8_t *packed_codes, float *scales, ui
                                                                                packed_codes, nbytes);
         DLLM_LAUNCH_CHECK();
     }
-    if (scales) DLLM_HIP_TRY(hipMemcpyAsync(scales, h->scales, h->G * h->N * 4, hipMemcpyDeviceToDevice, st));
-    if (zps) DLLM_HIP_TRY(hipMemcpyAsync(zps, h->zps, h->G * h->N, hipMemcpyDeviceToDevice, st));
+    if (scales || zps) {
+        dim3 gs(static_cast<unsigned>((h->N + 255) / 256), static_cast<unsigned>(h->G));
+        export_params_kernel<<<gs, 256, 0, st>>>(h->sf, h->sz, h->G, h->N, h->Npad, scales, zps);
+        DLLM_LAUNCH_CHECK();
+    }
     return DLLM_OK;
 }
 
@@ -2036,8 +2073,8 @@ size_t dllm_linear_weight_bytes(dllm_linear_t h) {
 
 size_t dllm_linear_device_bytes(dllm_linear_t h) {
     if (!h) return 0;
-    size_t b = h->Npad * h->K * h->bits / 8 + h->Npad * ((h->K + 127) / 128) * 128 * h->bits / 8   // wdev + wdec
-               + h->G * h->Npad * 8 + h->G * h->N * 5 + h->Npad * 4;                              // sz, sf, scales, zps, bias
+    size_t b = h->Npad * h->K * h->bits / 8 + h->G * h->Npad * 8 + h->Npad * 4;   // wdev, sz + sf, bias
+    if (h->wdec) b += h->Npad * ((h->K + 127) / 128) * 128 * h->bits / 8;          // decode layout, once built
 #if DLLM_LAB
     b += h->Npad * h->K * h->bits / 8;
 #endif

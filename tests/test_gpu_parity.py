@@ -477,12 +477,19 @@ def test_linear_exact_weights_tight(dllm, torch, orc, M, N, group):
 
 
 def test_linear_device_memory(dllm, torch):
-    """The handle keeps two code layouts (prefill and decode fragments, 8 MiB each at 4096^2 int4)
-    and the per-(group, column) parameters -- no canonical or A/B copies."""
+    """The handle keeps the prefill code layout (8 MiB at 4096^2 int4) and the per-(group, column)
+    parameters (sz pairs + f32 scales, 1 MiB) -- no canonical, scale/zp or A/B copies; the decode
+    layout (another 8 MiB) appears with the first M <= 64 call, which must then match a handle
+    whose decode layout was built first."""
     W = 0.02 * torch.randn(4096, 4096, device="cuda")
     lin = dllm.QuantLinear.from_weight(W, None, 4, 128)
     mib = lin.device_bytes() / 2**20
-    assert mib <= 17.75, mib
+    assert mib <= 9.05, mib
+    X = torch.randn(8, 4096, device="cuda").half()
+    y = lin(X)
+    mib2 = lin.device_bytes() / 2**20
+    assert 17.0 <= mib2 <= 17.05, mib2
+    assert torch.equal(lin(X), y)
     lin.close()
 
 
