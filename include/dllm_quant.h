@@ -212,7 +212,9 @@ int dllm_linear_create_quantized_ex(const uint8_t *packed_codes, const float *sc
  * through a workspace owned by the handle.  Shapes with too few output tiles to fill the GPU
  * (M roughly 65..1000 at N = 4096) split K into slices whose f32 partials are combined in slice
  * order (deterministic) through a per-(device, stream) workspace.  Both workspaces only grow and
- * are allocated on the first call that needs them, which therefore must precede stream capture. */
+ * are allocated on the first call that needs them, which therefore must precede stream capture;
+ * likewise the decode-fragment copy of the weights, built by the handle's first M <= 64 call
+ * (a capture-time first call returns DLLM_ERR_INVALID_PARAMS). */
 int dllm_linear_forward(dllm_linear_t h, const void *X, size_t M, int x_dtype, void *Y, int y_dtype,
                         dllm_stream_t stream);
 /* Export the quantized weights in canonical form (packed bitstream [K][N], scales [G][N], zps);
@@ -223,8 +225,9 @@ int dllm_linear_info(dllm_linear_t h, size_t *K, size_t *N, uint8_t *bits, size_
 int dllm_linear_precision(dllm_linear_t h);   /* DLLM_PRECISION_*, -1 on a null handle */
 /* HBM bytes the forward's GEMM kernel reads for the weights (packed codes + scales/zps). */
 size_t dllm_linear_weight_bytes(dllm_linear_t h);
-/* Device memory the handle owns (two code layouts -- prefill and decode fragments -- and the
- * per-(group, column) parameters; the X staging workspace once grown). */
+/* Device memory the handle owns: the prefill code layout and the per-(group, column) parameters
+ * (f16 zero-point/scale pairs + f32 scales) -- 9.02 MiB at 4096 x 4096 int4 g128 -- plus, once
+ * built, the decode code layout (+8 MiB there) and the X staging workspace once grown. */
 size_t dllm_linear_device_bytes(dllm_linear_t h);
 #ifdef DLLM_LAB
 /* Lab build only (libdllm_hip_lab.so): A/B schedule variants and ablation masks; mutates the

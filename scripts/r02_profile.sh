@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 OUT="$PWD/gpurun_out/prof2"
 mkdir -p "$OUT"
 KREGEX=${KREGEX:-wq_gemm_exact_kernel}
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu > "$OUT/kt.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu --no-denoise > "$OUT/kt.log" 2>&1
 rc=$?; echo "kernel-trace rc=$rc"; tail -2 "$OUT/kt.log"
 [ $rc -eq 0 ] || exit $rc
 for C in "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"; do
