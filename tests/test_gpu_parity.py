@@ -493,6 +493,34 @@ def test_linear_device_memory(dllm, torch):
     lin.close()
 
 
+def test_linear_decode_layout_refused_in_capture(dllm, torch):
+    """The decode layout is built by a handle's first M <= 64 call; a first call inside stream
+    capture must fail loudly (no allocation can be captured) rather than record a hipMalloc, and
+    the same call after capture ends must then build it and match a fresh handle."""
+    W = 0.02 * torch.randn(1024, 512, device="cuda")
+    lin = dllm.QuantLinear.from_weight(W, None, 4, 128)
+    X = torch.randn(4, 1024, device="cuda").half()
+    lin(torch.randn(256, 1024, device="cuda").half())     # prefill path only: grows the X workspace
+    s = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    raised = False
+    with torch.cuda.stream(s):
+        try:
+            with torch.cuda.graph(g, stream=s):
+                lin(X)
+        except Exception:           # the library's error, or the capture's invalidation after it
+            raised = True
+    torch.cuda.synchronize()
+    assert raised, "a first decode call inside capture must not succeed"
+    before = lin.device_bytes()
+    y = lin(X)
+    assert lin.device_bytes() == before + 512 * 1024 // 2      # the decode layout, built now
+    ref = dllm.QuantLinear.from_weight(W, None, 4, 128)
+    assert torch.equal(ref(X), y)
+    lin.close()
+    ref.close()
+
+
 @pytest.mark.lab
 @pytest.mark.parametrize("variant", [4, 8, 9, 10, 11, 14, 15])
 @pytest.mark.parametrize("bits", [2, 4, 8])
