@@ -476,6 +476,39 @@ def test_linear_exact_weights_tight(dllm, torch, orc, M, N, group):
     lin.close()
 
 
+@pytest.mark.parametrize("M,N,group", [(4096, 1024, 128), (4096, 512, 128), (1024, 4096, 128), (256, 4096, 256),
+                                       (65, 4096, 128), (300, 1280, 64), (129, 384, 128)])
+def test_linear_split_k_combine_repeatable(dllm, torch, orc, M, N, group):
+    """Shapes whose exact GEMM splits K (the slices are combined in slice order inside the launch by
+    the last-arriving block, counters left at zero): back-to-back calls into a NaN-filled output,
+    with the f32 and the fused-epilogue-free f16 outputs, must be bit-identical to each other and
+    within the exact-weights bound of the f32 product -- a counter left non-zero by a call would
+    leave the next call's output NaN, a stale slab read would break the bound."""
+    K = 4096 if N <= 1280 else 2048
+    g = torch.Generator(device="cuda").manual_seed(M + N)
+    W = 0.02 * torch.randn(K, N, device="cuda", generator=g)
+    b = 0.1 * torch.randn(N, device="cuda", generator=g)
+    X = torch.randn(M, K, device="cuda", generator=g).half()
+    lin = dllm.QuantLinear.from_weight(W, b, 4, group)
+    codes, scales, zps = lin.export()
+    outs = []
+    for rep in range(3):
+        Y = torch.full((M, N), float("nan"), device="cuda")
+        lin(X, out=Y)
+        outs.append(Y.clone())
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+    Wh = dev(torch, orc.dequantize_weights(orc.unpack_bits(host(codes), K * N, 4).reshape(K, N),
+                                           host(scales), host(zps), group))
+    Yr = X.float() @ Wh + b
+    rel = (torch.linalg.norm(outs[0] - Yr) / torch.linalg.norm(Yr)).item()
+    assert rel <= EXACT_TOL, rel
+    Y16 = torch.full((M, N), float("nan"), device="cuda", dtype=torch.float16)
+    lin(X, out=Y16)
+    assert torch.equal(Y16, outs[0].half())
+    lin.close()
+
+
 def test_linear_device_memory(dllm, torch):
     """The handle keeps the prefill code layout (8 MiB at 4096^2 int4) and the per-(group, column)
     parameters (sz pairs + f32 scales, 1 MiB) -- no canonical, scale/zp or A/B copies; the decode
