@@ -155,12 +155,15 @@ _lib = None
 
 def load(path: str | os.PathLike | None = None):
     """Loads libdllm_hip.so (raises if absent: there is no CPU fallback).  DLLM_LIB=lab selects the
-    lab build (measurement scripts only)."""
+    lab build, DLLM_LIB=<file> another build of the same ABI (measurement scripts only)."""
     global _lib
     if _lib is not None and path is None:
         return _lib
-    if path is None and os.environ.get("DLLM_LIB") == "lab":
+    env = os.environ.get("DLLM_LIB")
+    if path is None and env == "lab":
         path = LAB_LIB_PATH
+    elif path is None and env:      # measurement A/B: an explicit library file
+        path = env
     p = Path(path) if path else LIB_PATH
     if not p.exists():
         raise ImportError(f"{p} not built; run `python -c 'import __graft_entry__ as g; g.build()'` "
@@ -173,7 +176,7 @@ def load(path: str | os.PathLike | None = None):
         if hasattr(lib, name):
             fn = getattr(lib, name)
             fn.restype, fn.argtypes = res, args
-    if path is None or os.environ.get("DLLM_LIB") == "lab":
+    if path is None or (env and str(path) in (env, str(LAB_LIB_PATH))):
         _lib = lib
     return lib
 
