@@ -55,7 +55,12 @@ def parse():
     p.add_argument("--prewarm-ms", type=float, default=300.0,
                    help="untimed launches of the same step before the W warmup steps, so the clocks "
                         "have ramped before timing (outside the timed region)")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.tp_steps == 1:
+        # a 1-step schedule is the reference's degenerate linear schedule (0/0 in the beta ramp,
+        # lib.rs:554-593): its output is NaN by construction, so it measures nothing useful
+        p.error("--tp-steps must be 0 (skip) or >= 2")
+    return a
 
 
 def algorithmic_bytes(M, K, N, bits, group):
