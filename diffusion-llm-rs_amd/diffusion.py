@@ -373,14 +373,20 @@ class DenoiseLoop:
 
     overlap=True runs the work of a step that does not depend on x -- the KV-cache update (the
     simple model's update_kv_cache passes K/V through, lib.rs:826-835, and forward_with_cache
-    ignores them, :815-824) and the step's noise draw (dllm_randn into one of two buffers) -- on
-    a side stream while layers 0..L-2 run; the last layer waits only for its noise.  The result
-    is bit-identical to overlap=False."""
+    ignores them, :815-824) -- on a side stream while the layers run.  The step's noise is drawn
+    inside the last layer's fused p_sample epilogue (noise="epilogue", the default when the last
+    layer has forward_psample), or on the side stream into one of two buffers (noise="side"; the
+    last layer then waits for it).  Every form is bit-identical to overlap=False.  Measured at
+    config C5 (scripts/c5_ab.py): epilogue 0.922, side 0.953, serial 0.963 ms per step -- the
+    side-stream draw costs the GEMMs more CU time than the in-epilogue draw costs the last layer."""
 
     def __init__(self, layers: Sequence, config: DiffusionConfig, cumprod: Cumprod = Cumprod.INCLUSIVE,
                  alpha_mode: AlphaMode = AlphaMode.PER_SAMPLE, seed: int = 0,
-                 kv_cache: Optional[KVCacheEntry] = None, overlap: bool = True):
+                 kv_cache: Optional[KVCacheEntry] = None, overlap: bool = True, noise: str = "epilogue"):
+        if noise not in ("side", "epilogue"):
+            raise ValueError("noise must be 'side' or 'epilogue'")
         self.layers = list(layers)
+        self.noise_mode = noise if hasattr(self.layers[-1], "forward_psample") else "side"
         self.config = config
         self.cumprod, self.alpha_mode, self.seed = cumprod, alpha_mode, seed
         self.kv_cache = kv_cache
@@ -474,6 +480,12 @@ class DenoiseLoop:
         freed = [None, None]        # main-stream events: noise buffer j no longer read
         side.wait_stream(main)
         for i, t in enumerate(range(num_steps - 1, -1, -1)):
+            if self.noise_mode == "epilogue":      # noise drawn in the last layer's epilogue
+                with torch.cuda.stream(side):
+                    self.kv_step(t, num_steps)
+                buf = self.step(x, t, i, out=buf)
+                x, buf = buf, x
+                continue
             j = i % 2
             nz = self._noise[j]
             with torch.cuda.stream(side):
