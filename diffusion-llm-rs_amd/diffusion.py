@@ -386,7 +386,7 @@ class DenoiseLoop:
         if noise not in ("side", "epilogue"):
             raise ValueError("noise must be 'side' or 'epilogue'")
         self.layers = list(layers)
-        self.noise_mode = noise if hasattr(self.layers[-1], "forward_psample") else "side"
+        self.noise_mode = noise if self.layers and hasattr(self.layers[-1], "forward_psample") else "side"
         self.config = config
         self.cumprod, self.alpha_mode, self.seed = cumprod, alpha_mode, seed
         self.kv_cache = kv_cache
