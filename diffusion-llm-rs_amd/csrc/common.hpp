@@ -69,6 +69,12 @@ __device__ __forceinline__ void blds4_asm(__amdgpu_buffer_rsrc_t rs, uint32_t vo
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(voff), "s"(rs), "s"(lds_dst), "s"(soff) : "memory");
 }
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+// Buffer load of 16 B per lane into VGPRs from inline asm: like the LDS-DMA above, invisible to
+// hipcc's waitcnt pass -- the caller's counted vmcnt waits must cover it before d is read.
+__device__ __forceinline__ void bload16_asm(u32x4_t &d, __amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff) {
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(d) : "v"(voff), "s"(rs), "s"(soff) : "memory");
+}
 // Raw buffer descriptor over [base, base + 4 GiB) (no range clamp is relied on).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t raw_rsrc(const void *base) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, 0x7FFFFFFF, 0x00020000);

@@ -23,6 +23,31 @@
 #ifndef DLLM_LAB
 #define DLLM_LAB 0
 #endif
+// Policy switches (product defaults; A/B builds flip them, profiles/r02_gemm_ab/):
+// DLLM_EXACT_WREG = 1: int4 weight words go global -> VGPR (buffer_load_dwordx4 from inline asm,
+//   counted in the same vmcnt waits as the stage's LDS-DMA) instead of through the LDS ring: each
+//   wave's slab words are its own (bit-identical; -0.5 %, and 16 KiB less LDS per stage).
+// DLLM_EXACT_KG2 = 1: tile-starved grids (column shards) run 128 x 128 or 64 x 128 tiles with two
+//   k-groups of 4 waves per block (4096 x 1024: 45.0 -> 40.5 us; 4096 x 512: 32.0 -> 24.4 us).
+// DLLM_EXACT_MR2 = 1: grids still short of a round get 64 x 128 tiles (two blocks per CU).
+// DLLM_EXACT_PRIO = 0 drops the s_setprio raise around the MFMA sections (measured 1 % slower).
+// DLLM_EXACT_RING2 = 1: two groups per stage in a 2-stage ring (one barrier per two groups):
+//   spills at 256 VGPRs, not adopted (a build without the per-stage barrier is only 8 % faster).
+#ifndef DLLM_EXACT_WREG
+#define DLLM_EXACT_WREG 1
+#endif
+#ifndef DLLM_EXACT_PRIO
+#define DLLM_EXACT_PRIO 1
+#endif
+#ifndef DLLM_EXACT_MR2
+#define DLLM_EXACT_MR2 1
+#endif
+#ifndef DLLM_EXACT_RING2
+#define DLLM_EXACT_RING2 0
+#endif
+#ifndef DLLM_EXACT_KG2
+#define DLLM_EXACT_KG2 1
+#endif
 
 #include <algorithm>
 #include <type_traits>
@@ -33,16 +58,16 @@ namespace {
 
 // A stage holds SPS consecutive 64-deep slabs (X tile, weight words) plus the group's zero-point
 // pairs and f32 scales; SPS = 2 makes a stage one 128-row group (one fold and one barrier per group).
-template <int BITS, int NW, int MR, int SPS>
+template <int BITS, int NW, int MR, int SPS, bool WREG = false, int GPS = 1>
 struct ExactStage {
     static constexpr int kR1 = 4 * MR / NW;                // 1-KiB X pieces per wave per slab
     static constexpr int kXRounds = SPS * kR1;
     static constexpr int kX1 = 32 * MR * kBK * 2;           // one slab's X tile [32 MR][64] f16
     static constexpr int kX = SPS * kX1;
     static constexpr int kW1 = NW * 64 * BITS * 4;          // one slab's weight words
-    static constexpr int kW = SPS * kW1;
-    static constexpr int kSZ = 1024;                        // u32 {-(1024+zp)} pairs, 32 NW columns (+ mirror)
-    static constexpr int kSF = 1024;                        // f32 scales, 32 NW columns (+ mirror)
+    static constexpr int kW = WREG ? 0 : SPS * kW1;   // WREG: the words live in VGPRs
+    static constexpr int kSZ = 1024 * GPS;                  // u32 {-(1024+zp)} pairs, 32 NW columns (+ mirror) per group
+    static constexpr int kSF = 1024 * GPS;                  // f32 scales, 32 NW columns (+ mirror) per group
     static constexpr int kBytes = kX + kW + kSZ + kSF;
     static constexpr int kWOps = SPS * (BITS == 4 ? 1 : 2);
     static_assert(kR1 >= 1 && 4 * MR % NW == 0, "X staging must split evenly over the waves");
@@ -54,18 +79,28 @@ struct ExactStage {
 // that rep's fold with the group's scales -- so only 2 transient accumulators are live (a 128 + 256
 // register budget does not fit at two waves per SIMD).  Folding per 64-deep slab instead of per
 // group is the same sum: both slabs of a group carry the same scale.
+// GPS > 1 (KPG = 1): a stage holds GPS whole groups (group = 64 SPS / GPS), folded inside the stage.
+// RING: LDS stages in the ring (3: stage kt + 2 issued while kt computes; 2: stage kt + 1, one
+// barrier per stage -- with GPS = 2 one barrier per two groups).
+// KG = 2: two k-groups of NW waves share the block's tile, k-group g taking the g-th half of the
+// slice's stages (own LDS stage parts, same barriers); their sums are added in the epilogue,
+// k-group 0's first: a tile-starved grid gets two waves per SIMD without a second launch.
 template <int BITS, typename YT, int NW, int MR, int SPS, int KPG, bool SPLIT = false, int EPI = 0, bool TM = false,
-          int TMB = 1>
-__global__ void __launch_bounds__(NW * 64, NW == 8 ? 1 : 2)
+          int TMB = 1, bool WREG = false, int GPS = 1, int RING = 3, int KG = 1>
+__global__ void __launch_bounds__(NW * KG * 64, NW * KG == 8 ? 1 : 2)
 wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdev,
                      const uint32_t *__restrict__ sz, const float *__restrict__ sf, const float *__restrict__ bias,
                      YT *__restrict__ Y, int N, int Npad, int group, int nbm, int nbn, int nsplit = 1,
                      float *__restrict__ ws = nullptr, PSampleEpi epi = PSampleEpi{}) {
-    using SL = ExactStage<BITS, NW, MR, SPS>;
+    using SL = ExactStage<BITS, NW, MR, SPS, WREG, GPS>;
+    static_assert(!WREG || (BITS == 4 && !TM), "register-staged weight words: int4, group-major stages");
+    static_assert(GPS == 1 || (KPG == 1 && !TM && (4 * SPS) % GPS == 0 && 2 * GPS <= NW), "whole groups per stage");
+    static_assert(RING == 3 || (RING == 2 && !TM), "ring depth");
+    static_assert(KG == 1 || (!TM && RING * KG * SL::kBytes >= NW * 64 * MR * 16 * 4), "k-group combine fits the ring");
     constexpr int kBMt = 32 * MR, kBNt = 32 * NW;
-    __shared__ __attribute__((aligned(16))) uint8_t st0[SL::kBytes];
-    __shared__ __attribute__((aligned(16))) uint8_t st1[SL::kBytes];
-    __shared__ __attribute__((aligned(16))) uint8_t st2[SL::kBytes];
+    // RING stages of KG parts each (k-group g's part of stage i at ring + (i KG + g) kBytes)
+    __shared__ __attribute__((aligned(16))) uint8_t ring[RING * KG * SL::kBytes];
+    uint8_t *const st0 = ring, *const st1 = ring + KG * SL::kBytes, *const st2 = ring + 2 * KG * SL::kBytes;
 
     // XCD-aware order: consecutive work items land on one XCD (blocks b, b+8 share an XCD under
     // round-robin dispatch); K-slice outermost so an XCD's blocks share the slice's X rows in L2.
@@ -82,11 +117,14 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
     const int bm = first + in_grp % gm, bn = in_grp / gm;
 
     const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int kg = KG == 1 ? 0 : __builtin_amdgcn_readfirstlane((tid >> 6) / NW);
+    const int wave = __builtin_amdgcn_readfirstlane((tid >> 6) - kg * NW);   // wave within the k-group
     const int m0 = bm * kBMt, n0 = bn * kBNt;
     const unsigned nk_all = static_cast<unsigned>(K) / kBK;                 // 64-deep slabs
-    const unsigned nk = nk_all / SPS / static_cast<unsigned>(nsplit);       // stages of this slice
-    const unsigned kt0 = static_cast<unsigned>(ks) * nk;
+    const unsigned nk_slice = nk_all / SPS / static_cast<unsigned>(nsplit); // stages of this slice
+    const unsigned nk = nk_slice / KG;                                      // stages of this k-group
+    const unsigned kt0 = static_cast<unsigned>(ks) * nk_slice + static_cast<unsigned>(kg) * nk;
+    const uint32_t kpart = static_cast<uint32_t>(kg) * SL::kBytes;          // this k-group's part of a stage
     const unsigned spg = static_cast<unsigned>(group) / kBK;                // slabs per group
     const unsigned nt = static_cast<unsigned>(n0 + wave * 32) >> 5;
 
@@ -105,8 +143,9 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
     const __amdgpu_buffer_rsrc_t wrs = raw_rsrc(wdev + static_cast<size_t>(nt) * nk_all * 64 * BITS);
     const uint32_t woff = static_cast<uint32_t>(lane * BITS * 4);
     const int ncol = lane & (8 * NW - 1);                    // 4 columns per lane (NW = 4: lanes 32.. mirror)
-    const bool has_sz = wave == 0, has_sf = wave == 1;
-    // wave 0 stages the zero-point pairs, wave 1 the f32 scales: the same byte offsets in two arrays
+    // waves 2g / 2g + 1 stage group g's zero-point pairs / f32 scales: the same byte offsets in two arrays
+    const int pg = wave >> 1;
+    const bool has_sz = wave < 2 * GPS && (wave & 1) == 0, has_sf = wave < 2 * GPS && (wave & 1) == 1;
     const __amdgpu_buffer_rsrc_t prs = raw_rsrc(has_sz ? static_cast<const void *>(sz + n0) : static_cast<const void *>(sf + n0));
     const uint32_t poff = static_cast<uint32_t>(16 * ncol);
     const uint32_t wv = static_cast<uint32_t>(wave);
@@ -114,7 +153,10 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
     // LDS destinations go through readfirstlane: the M0 operand must be an SGPR, and hipcc's
     // divergence analysis does not prove it uniform through the unrolled ring.
     auto u = [](uint32_t v) { return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(v))); };
-    auto stage = [&](uint8_t *sb, unsigned kt) __attribute__((always_inline)) {
+    // WREG: ring slot r's weight words (one 16-B load per lane per 64-deep slab).
+    u32x4_t wq[RING][SPS];
+    auto stage = [&](uint8_t *sb, unsigned kt, auto slot_tag) __attribute__((always_inline)) {
+        constexpr int slot = decltype(slot_tag)::value;
         const uint32_t base = u(lds_addr(sb));
         const unsigned slab0 = (kt + kt0) * SPS;
 #pragma unroll
@@ -126,7 +168,9 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
         for (int s = 0; s < SPS; ++s) {
             const uint32_t so = u((slab0 + s) * 64 * BITS * 4);
             const uint32_t wb = u(base + SL::kX + s * SL::kW1 + wv * (64 * BITS * 4));
-            if constexpr (BITS == 4) {
+            if constexpr (WREG) {
+                bload16_asm(wq[slot][s], wrs, woff, so);
+            } else if constexpr (BITS == 4) {
                 blds16_asm(wrs, woff, so, wb);
             } else if constexpr (BITS == 8) {
                 blds16_asm(wrs, woff, so, wb);
@@ -136,13 +180,14 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
                 blds4_asm(wrs, lane * 8 + 4, so, u(wb + 256));
             }
         }
-        const uint32_t goff = u((slab0 / spg) * static_cast<uint32_t>(Npad) * 4);
-        if (has_sz) blds16_asm(prs, poff, goff, u(base + SL::kX + SL::kW));
-        if (has_sf) blds16_asm(prs, poff, goff, u(base + SL::kX + SL::kW + SL::kSZ));
+        const uint32_t goff = u((slab0 / spg + pg) * static_cast<uint32_t>(Npad) * 4);
+        if (has_sz) blds16_asm(prs, poff, goff, u(base + SL::kX + SL::kW + pg * 1024));
+        if (has_sf) blds16_asm(prs, poff, goff, u(base + SL::kX + SL::kW + SL::kSZ + pg * 1024));
     };
     // Counted wait leaving the newest stage's DMAs (this wave's own count) in flight.
     auto wait_prev = [&]() __attribute__((always_inline)) {
-        if (has_sz || has_sf) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kXRounds + SL::kWOps + 1) : "memory");
+        if constexpr (RING == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else if (has_sz || has_sf) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kXRounds + SL::kWOps + 1) : "memory");
         else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kXRounds + SL::kWOps) : "memory");
     };
 
@@ -168,28 +213,47 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
 
     // One stage (SPS slabs) on sb; stage pf receives stage kt + 2.  GF: first stage of a group (the
     // group's first MFMA starts from zero); GL: last (fold the group into acc with its scales).
-    auto step = [&](const uint8_t *sb, uint8_t *pf, unsigned kt, auto gf_tag, auto gl_tag) __attribute__((always_inline)) {
+    auto step = [&](const uint8_t *sb, uint8_t *pf, unsigned kt, auto gf_tag, auto gl_tag, auto cur_tag) __attribute__((always_inline)) {
         constexpr bool GF = decltype(gf_tag)::value, GL = decltype(gl_tag)::value;
-        constexpr int kSub = 4 * SPS;
-        const bool issue = kt + 2 < nk;
-        if (issue) stage(pf, kt + 2);
+        constexpr int cur = decltype(cur_tag)::value;
+        constexpr int kSub = 4 * SPS, kSubG = kSub / GPS;
         uint32_t w[SPS][BITS];
+        if constexpr (WREG) {
+            // This slot's loads landed before the previous step's barrier (counted vmcnt); the empty
+            // asm redefines the words after that wait, so no use of them can be scheduled above it.
 #pragma unroll
-        for (int s = 0; s < SPS; ++s) lds_words<BITS>(w[s], sb + SL::kX + s * SL::kW1 + wave * (64 * BITS * 4), lane);
-        const half2_t p = __builtin_bit_cast(half2_t,
-                                             *reinterpret_cast<const uint32_t *>(sb + SL::kX + SL::kW + (wave * 32 + (lane & 31)) * 4));
-        const ExactConsts ec = exact_consts(half2_t{p[0], p[0]});
+            for (int s = 0; s < SPS; ++s) {
+                asm volatile("" : "+v"(wq[cur][s]));
+#pragma unroll
+                for (int j = 0; j < BITS; ++j) w[s][j] = wq[cur][s][j];
+            }
+        }
+        const bool issue = kt + RING - 1 < nk;
+        if (issue) stage(pf, kt + RING - 1, std::integral_constant<int, (cur + RING - 1) % RING>{});
+        if constexpr (!WREG) {
+#pragma unroll
+            for (int s = 0; s < SPS; ++s) lds_words<BITS>(w[s], sb + SL::kX + s * SL::kW1 + wave * (64 * BITS * 4), lane);
+        }
+        ExactConsts ec[GPS];
+#pragma unroll
+        for (int g = 0; g < GPS; ++g) {
+            const half2_t p = __builtin_bit_cast(
+                half2_t, *reinterpret_cast<const uint32_t *>(sb + SL::kX + SL::kW + g * 1024 + (wave * 32 + (lane & 31)) * 4));
+            ec[g] = exact_consts(half2_t{p[0], p[0]});
+        }
         half8_t bA[MR], bB[MR];
         read_b(bA, sb, 0);
-        half8_t aA = dequant_exact<BITS>(w[0], 0, ec), aB;
-        // Scales of this group (lane half hsel holds columns 4 hsel + 8 qd + (0..3) of the wave's 32),
-        // read at the head of the stage so the fold never waits on LDS.
+        half8_t aA = dequant_exact<BITS>(w[0], 0, ec[0]), aB;
+        // Scales of a group (lane half hsel holds columns 4 hsel + 8 qd + (0..3) of the wave's 32): GPS = 1
+        // reads them at the head of the stage so the fold never waits on LDS; GPS > 1 at the head of
+        // each group's last substep.
         float4 s4[4];
-        if constexpr (GL) {
-            const float *sfl = reinterpret_cast<const float *>(sb + SL::kX + SL::kW + SL::kSZ) + wave * 32 + 4 * hsel;
+        auto read_s4 = [&](int g) __attribute__((always_inline)) {
+            const float *sfl = reinterpret_cast<const float *>(sb + SL::kX + SL::kW + SL::kSZ + g * 1024) + wave * 32 + 4 * hsel;
 #pragma unroll
             for (int qd = 0; qd < 4; ++qd) s4[qd] = *reinterpret_cast<const float4 *>(sfl + 8 * qd);
-        }
+        };
+        if constexpr (GL && GPS == 1) read_s4(0);
         // acc[r] += s (.) T_g[r]
         auto fold = [&](int r) __attribute__((always_inline)) {
 #pragma unroll
@@ -202,14 +266,35 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
         };
         auto sub = [&](half8_t (&bc)[MR], half8_t (&bn)[MR], const half8_t &ac, half8_t &an, auto v_tag) __attribute__((always_inline)) {
             constexpr int v = decltype(v_tag)::value;
+            // first / last substep of a group (GPS > 1: inside the stage; else the stage's tags)
+            constexpr bool gfirst = GPS > 1 ? v % kSubG == 0 : (GF && v == 0);
+            constexpr bool glast = GPS > 1 ? v % kSubG == kSubG - 1 : (GL && v == kSub - 1);
             __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_setprio(1);
-            if constexpr (v + 1 < kSub) {
+            if constexpr (DLLM_EXACT_PRIO) __builtin_amdgcn_s_setprio(1);
+            if constexpr (GPS > 1 && glast) read_s4(v / kSubG);
+            if constexpr (GPS > 1 && glast && v + 1 < kSub) {
+                // A group's last substep with the next group's first in the same stage: prefetch the
+                // next fragments and fold this group beside its last MFMAs.
                 read_b(bn, sb, v + 1);
-                an = dequant_exact<BITS>(w[(v + 1) / 4], (v + 1) % 4, ec);
+                an = dequant_exact<BITS>(w[(v + 1) / 4], (v + 1) % 4, ec[(v + 1) / kSubG]);
 #pragma unroll
                 for (int r = 0; r < MR; ++r)
-                    tacc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bc[r], (GF && v == 0) ? zero16 : tacc[r], 0, 0, 0);
+                    tacc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bc[r], gfirst ? zero16 : tacc[r], 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < MR; ++r) fold(r);
+#pragma unroll
+                for (int i = 0; i < MR; ++i) {
+                    if (i >= 2) __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);   // fold of rep i - 2
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);               // MFMA rep i
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);               // DS read
+                    __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);               // dequant
+                }
+            } else if constexpr (v + 1 < kSub) {
+                read_b(bn, sb, v + 1);
+                an = dequant_exact<BITS>(w[(v + 1) / 4], (v + 1) % 4, ec[(v + 1) / kSubG]);
+#pragma unroll
+                for (int r = 0; r < MR; ++r)
+                    tacc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bc[r], gfirst ? zero16 : tacc[r], 0, 0, 0);
 #pragma unroll
                 for (int i = 0; i < MR; ++i) {
                     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
@@ -221,8 +306,8 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
                 // beside the group's own last MFMAs instead of after all of them.
 #pragma unroll
                 for (int r = 0; r < MR; ++r)
-                    tacc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bc[r], (GF && v == 0) ? zero16 : tacc[r], 0, 0, 0);
-                if constexpr (GL) {
+                    tacc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bc[r], gfirst ? zero16 : tacc[r], 0, 0, 0);
+                if constexpr (glast) {
 #pragma unroll
                     for (int r = 0; r < MR; ++r) fold(r);
                     __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // MFMA r = 0, 1
@@ -233,14 +318,14 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
                     }
                 }
             }
-            __builtin_amdgcn_s_setprio(0);
+            if constexpr (DLLM_EXACT_PRIO) __builtin_amdgcn_s_setprio(0);
             __builtin_amdgcn_sched_barrier(0);
         };
         [&]<int... Vs>(std::integer_sequence<int, Vs...>) __attribute__((always_inline)) {
             ((Vs % 2 == 0 ? sub(bA, bB, aA, aB, std::integral_constant<int, Vs>{})
                           : sub(bB, bA, aB, aA, std::integral_constant<int, Vs>{})), ...);
         }(std::make_integer_sequence<int, kSub>{});
-        // Stage kt+1 must have landed; kt+2's DMAs may stay in flight across the barrier.
+        // Stage kt+1 must have landed; (RING 3) kt+2's DMAs may stay in flight across the barrier.
         if (issue) wait_prev();
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -249,7 +334,7 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
     };
     auto step_tm = [&](const uint8_t *sb, uint8_t *pf, unsigned kt) __attribute__((always_inline)) {
         const bool issue = kt + 2 < nk;
-        if (issue) stage(pf, kt + 2);
+        if (issue) stage(pf, kt + 2, std::integral_constant<int, 0>{});
         uint32_t w[BITS];
         lds_words<BITS>(w, sb + SL::kX + wave * (64 * BITS * 4), lane);
         const half2_t p = __builtin_bit_cast(half2_t,
@@ -312,19 +397,23 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
     // dispatch made hipcc spill ~80 VGPRs).
     auto at = [&](auto i_tag, unsigned kt) __attribute__((always_inline)) {
         constexpr int I = decltype(i_tag)::value;
-        constexpr int cur = I % 3, nxt = (I + 2) % 3;
-        uint8_t *sb = cur == 0 ? st0 : (cur == 1 ? st1 : st2);
-        uint8_t *pf = nxt == 0 ? st0 : (nxt == 1 ? st1 : st2);
+        constexpr int cur = I % RING, nxt = (I + RING - 1) % RING;
+        uint8_t *sb = (cur == 0 ? st0 : (cur == 1 ? st1 : st2)) + kpart;
+        uint8_t *pf = (nxt == 0 ? st0 : (nxt == 1 ? st1 : st2)) + kpart;
         if constexpr (TM) step_tm(sb, pf, kt);
         else step(sb, pf, kt, std::integral_constant<bool, I % KPG == 0>{},
-                  std::integral_constant<bool, I % KPG == KPG - 1>{});
+                  std::integral_constant<bool, I % KPG == KPG - 1>{}, std::integral_constant<int, cur>{});
     };
-    constexpr int kUnroll = (KPG == 1 || TM) ? 3 : (KPG == 2 ? 6 : 12);
+    constexpr int kUnroll = RING == 2 ? (KPG == 1 ? 2 : 4) : ((KPG == 1 || TM) ? 3 : (KPG == 2 ? 6 : 12));
 
-    stage(st0, 0);
-    if (nk > 1) stage(st1, 1);
-    if (nk > 1) wait_prev();
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stage(st0 + kpart, 0, std::integral_constant<int, 0>{});
+    if constexpr (RING == 3) {
+        if (nk > 1) stage(st1 + kpart, 1, std::integral_constant<int, 1>{});
+        if (nk > 1) wait_prev();
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     for (unsigned kt = 0; kt < nk; kt += kUnroll) {
@@ -333,6 +422,26 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
         }(std::make_integer_sequence<int, kUnroll>{});
     }
 
+    if constexpr (KG == 2) {
+        // k-group 1 hands its sums to k-group 0 through the (drained) ring: 16 B per lane per store.
+        float4 *xch = reinterpret_cast<float4 *>(ring) + (wave * MR * 4) * 64 + lane;
+        if (kg == 1) {
+#pragma unroll
+            for (int r = 0; r < MR; ++r)
+#pragma unroll
+                for (int qd = 0; qd < 4; ++qd)
+                    xch[(r * 4 + qd) * 64] = make_float4(acc[r][4 * qd], acc[r][4 * qd + 1], acc[r][4 * qd + 2], acc[r][4 * qd + 3]);
+        }
+        __syncthreads();
+        if (kg == 1) return;
+#pragma unroll
+        for (int r = 0; r < MR; ++r)
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd) {
+                const float4 o = xch[(r * 4 + qd) * 64];
+                acc[r][4 * qd] += o.x; acc[r][4 * qd + 1] += o.y; acc[r][4 * qd + 2] += o.z; acc[r][4 * qd + 3] += o.w;
+            }
+    }
     // Epilogue: acc[r] reg e -> n = n0 + 32 wave + 4 hsel + 8 (e >> 2) + (e & 3), m = m0 + 32 r + (lane & 31).
     const int nb0 = n0 + wave * 32 + 4 * hsel;
     if constexpr (SPLIT) {
@@ -391,21 +500,22 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
     }
 }
 
-template <int BITS, typename YT, int NW, int MR, int SPS, int KPG, int EPI, bool TM = false>
+template <int BITS, typename YT, int NW, int MR, int SPS, int KPG, int EPI, bool TM = false, int GPS = 1, int RING = 3,
+          int KG = 1, bool WREG = (DLLM_EXACT_WREG != 0 && BITS == 4 && !TM)>
 int launch_exact_tile(const ExactGemmArgs &a, int nsplit, hipStream_t st) {
     const int nbm = (a.M + 32 * MR - 1) / (32 * MR), nbn = a.Npad / (32 * NW);
     const unsigned nb = static_cast<unsigned>(nbm * nbn * nsplit);
     const PSampleEpi ep = a.epi ? *a.epi : PSampleEpi{};
     YT *Y = static_cast<YT *>(a.Y);
     if (nsplit == 1) {
-        wq_gemm_exact_kernel<BITS, YT, NW, MR, SPS, KPG, false, EPI, TM><<<nb, NW * 64, 0, st>>>(
+        wq_gemm_exact_kernel<BITS, YT, NW, MR, SPS, KPG, false, EPI, TM, 1, WREG, GPS, RING, KG><<<nb, NW * KG * 64, 0, st>>>(
             a.X, a.M, a.K, a.wdev, a.sz, a.sf, a.bias, Y, a.N, a.Npad, a.group, nbm, nbn, 1, nullptr, ep);
         DLLM_LAUNCH_CHECK();
         return DLLM_OK;
     }
     float *ws = device_workspace(st, static_cast<size_t>(nsplit) * a.M * a.Npad * sizeof(float));
     if (!ws) return DLLM_ERR_HIP;
-    wq_gemm_exact_kernel<BITS, YT, NW, MR, SPS, KPG, true, 0, TM><<<nb, NW * 64, 0, st>>>(
+    wq_gemm_exact_kernel<BITS, YT, NW, MR, SPS, KPG, true, 0, TM, 1, WREG, GPS, RING, KG><<<nb, NW * KG * 64, 0, st>>>(
         a.X, a.M, a.K, a.wdev, a.sz, a.sf, a.bias, Y, a.N, a.Npad, a.group, nbm, nbn, nsplit, ws);
     DLLM_LAUNCH_CHECK();
     const size_t q = static_cast<size_t>(a.M) * (a.Npad / 4);
@@ -415,9 +525,13 @@ int launch_exact_tile(const ExactGemmArgs &a, int nsplit, hipStream_t st) {
     return DLLM_OK;
 }
 
-// Tile policy: 128 x 256 tiles (8 waves, two per SIMD; stages of one 128-row group) when they give
-// >= 256 blocks; otherwise 128 x 128 tiles (4 waves, two blocks per CU, 64-deep stages) with K
-// split over group-aligned slices until the grid has >= ~200 blocks.  G64 = group / 64.
+// Tile policy (G64 = group / 64):
+// 1. 128 x 256 tiles (8 waves, two per SIMD; stages of one 128-row group) when they give >= 256 blocks;
+// 2. (int4, group 128, KG2) 128 x 128 tiles with two k-groups per block when those give 256..511
+//    blocks, else 64 x 128 tiles with two k-groups when those give >= 256;
+// 3. (MR2) 64 x 128 tiles (4 waves) while 128 x 128 tiles give < 512 blocks, K split until >= 512;
+// 4. 128 x 128 tiles (4 waves, two blocks per CU, 64-deep stages) with K split over group-aligned
+//    slices until the grid has >= ~200 blocks.
 template <int BITS, typename YT, int G64, int EPI>
 int launch_exact_bits(const ExactGemmArgs &a, hipStream_t st) {
     const int mb = (a.M + 127) / 128;
@@ -428,9 +542,31 @@ int launch_exact_bits(const ExactGemmArgs &a, hipStream_t st) {
     if (a.Npad % 256 == 0 && mb * (a.Npad / 256) >= kCUs) {
         // int8 weights: one-slab stages (two-slab stages exceed the 160 KiB LDS ring)
         if constexpr (G64 == 1 || BITS == 8) return launch_exact_tile<BITS, YT, 8, 4, 1, G64, EPI>(a, 1, st);
+#if DLLM_EXACT_RING2
+        // two whole 128-row groups per stage, 2-stage ring: one barrier per two groups
+        else if constexpr (G64 == 2 && BITS == 4 && DLLM_EXACT_WREG) return launch_exact_tile<BITS, YT, 8, 4, 4, 1, EPI, false, 2, 2>(a, 1, st);
+#endif
         else return launch_exact_tile<BITS, YT, 8, 4, 2, G64 / 2, EPI>(a, 1, st);
     }
     const int tiles = mb * (a.Npad / 128), ngroups = a.K / a.group;
+#if DLLM_EXACT_KG2
+    // tile-starved grids: 128 x 128 (or 64 x 128) tiles with two k-groups of 4 waves per block
+    if constexpr (G64 == 2 && BITS == 4 && DLLM_EXACT_WREG) {
+        if (tiles >= kCUs && tiles < 2 * kCUs && ngroups % 2 == 0)
+            return launch_exact_tile<BITS, YT, 4, 4, 2, 1, EPI, false, 1, 2, 2>(a, 1, st);
+        const int t64 = ((a.M + 63) / 64) * (a.Npad / 128);
+        if (tiles < kCUs && t64 >= kCUs && ngroups % 2 == 0)
+            return launch_exact_tile<BITS, YT, 4, 2, 2, 1, EPI, false, 1, 2, 2>(a, 1, st);
+    }
+#endif
+#if DLLM_EXACT_MR2
+    if (tiles < 2 * kCUs) {
+        const int t64 = ((a.M + 63) / 64) * (a.Npad / 128);
+        int ns = 1;
+        while (t64 * ns < 2 * kCUs && ns < 8 && ngroups % (2 * ns) == 0 && (a.K / kBK) / (2 * ns) >= 4) ns *= 2;
+        return launch_exact_tile<BITS, YT, 4, 2, 1, G64, EPI>(a, ns, st);
+    }
+#endif
     int nsplit = 1;
     while (tiles * nsplit < 200 && nsplit < 8 && ngroups % (2 * nsplit) == 0 && (a.K / kBK) / (2 * nsplit) >= 4)
         nsplit *= 2;
