@@ -6,7 +6,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT="$PWD/gpurun_out/r02_final"
+OUT="$PWD/gpurun_out/${RECORD:-r02_final}"
 mkdir -p "$OUT"
 hard() { case $1 in 124|134|137|139) return 0;; *) return 1;; esac; }
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \

@@ -5,7 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT="$PWD/gpurun_out/prof2"
+OUT="$PWD/gpurun_out/${PROF_OUT:-prof2}"
 mkdir -p "$OUT"
 KREGEX=${KREGEX:-wq_gemm_exact_kernel}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu --no-denoise > "$OUT/kt.log" 2>&1
