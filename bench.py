@@ -112,6 +112,33 @@ def cpu_baseline(K, N, bits, group, M, budget_s):
             "host_cpu": _cpu_model(), "nproc": os.cpu_count(), "all_cores": all_cores}
 
 
+def cpu_denoise_step(dm=4096, M=2048, L=12, bits=4, group=128):
+    """SURVEY.md 8d's C5 CPU plan: one denoise step of the reference path on the host = L layers of
+    (a2 dequant + f32 sgemm of M tokens x dm^2 + b) + p_sample; one layer is timed on 1 thread and on
+    the job's host-core share and multiplied by L (the elementwise p_sample is < 0.1 % of a layer and
+    not timed): labelled an extrapolation."""
+    from oracle import oracle as orc
+    rng = np.random.default_rng(1)
+    W = (0.02 * rng.standard_normal((dm, dm))).astype(np.float32)
+    codes, scales, zps = orc.quantize_weights(W, bits, group)
+    t0 = time.perf_counter()
+    What = orc.dequantize_weights(codes, scales, zps, group)
+    t_deq = time.perf_counter() - t0
+    b = np.zeros(dm, np.float32)
+    X = rng.standard_normal((M, dm)).astype(np.float32)
+    res = {}
+    for threads in (1, max(1, min(16, os.cpu_count() or 1))):
+        orc.sgemm_blocked(X[:64], What, b, nthreads=threads)
+        t0 = time.perf_counter()
+        orc.sgemm_blocked(X, What, b, nthreads=threads)
+        t_layer = t_deq + time.perf_counter() - t0
+        res[f"{threads}_threads"] = {"ms_per_step": round(1e3 * L * t_layer, 1),
+                                     "tok_per_s_per_step": M / (L * t_layer)}
+    res["sample"] = (f"one layer (a2 dequant + blocked AVX2 sgemm {M}x{dm}x{dm} + b) timed per thread count, "
+                     f"x {L} layers = one denoise step (extrapolated; p_sample not timed)")
+    return res
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -373,6 +400,8 @@ def main():
         out["m_sweep"] = m_sweep(lin, K, N, args.bits, args.group, torch, dev, stream)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(K, N, args.bits, args.group, M, args.cpu_seconds)
+        if "denoise_loop" in out:
+            out["denoise_loop"]["cpu_baseline"] = cpu_denoise_step()
     if rank == 0:
         print(json.dumps(out), flush=True)
     lin.close()
