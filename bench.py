@@ -198,6 +198,19 @@ def denoise_loop(d, torch, dev, steps=50):
     return res
 
 
+class _ComputeOnlyPair:
+    """A TensorParallelPair's two local GEMMs without its reduction: times the sharded loop's compute
+    alone (report compute-only and end-to-end scaling separately; the values are the
+    rank's un-reduced partials, so only the timing means anything)."""
+
+    def __init__(self, pair):
+        self.pair = pair
+
+    def __call__(self, x, out_dtype=None):
+        y = self.pair.partial(x)
+        return y if out_dtype is None or y.dtype == out_dtype else y.to(out_dtype)
+
+
 def denoise_loop_tp(d, torch, dist, dev, world, steps):
     """Config C5 hidden-dim sharded over the job's ranks: 12 int4 layers as 6
     Megatron pairs (parallel.TensorParallelPair: column shard, row shard, one reduction of the f32
@@ -206,7 +219,8 @@ def denoise_loop_tp(d, torch, dist, dev, world, steps):
     with a barrier and synchronize on both sides, max over ranks: "allreduce" (f32 all_reduce, then
     bias + f16 cast) and "rs_ag" (f32 reduce_scatter over token rows, cast on the local rows, f16
     all_gather: 3/4 of the bytes), each unchunked and with the reduction split into 4 token chunks
-    that overlap the next chunk's GEMM."""
+    that overlap the next chunk's GEMM.  "compute_only": the same loop with each pair's reduction
+    left out (the GEMMs, casts and p_sample only)."""
     par = d.parallel
     dm, M, L = 4096, 2048, 12
     res = {"workload": f"C5 hidden-dim sharded: {L // 2} TensorParallelPair of int4-g128 d{dm}, seq {M}, "
@@ -239,6 +253,22 @@ def denoise_loop_tp(d, torch, dist, dev, world, steps):
             key = f"{mode}_chunks{chunks}"
             res[key] = {"ms_per_step": round(s / steps * 1e3, 4), "tok_per_s_per_step": round(M / (s / steps), 1),
                         "finite": bool(torch.isfinite(out).all())}
+        if mode == "allreduce":
+            loop_c = d.DenoiseLoop([_ComputeOnlyPair(p) for p in pairs], cfg, cumprod=d.Cumprod.INCLUSIVE, seed=1,
+                                   kv_cache=None, overlap=False)
+            loop_c.sample(x, 2)
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            loop_c.sample(x, steps)
+            torch.cuda.synchronize()
+            dist.barrier()
+            t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            s = float(t.item())
+            res["compute_only"] = {"ms_per_step": round(s / steps * 1e3, 4),
+                                   "tok_per_s_per_step": round(M / (s / steps), 1),
+                                   "note": "the pairs' local GEMMs + casts + p_sample, no reduction (timing only)"}
         for p in pairs:
             p.close()
     return res
