@@ -33,6 +33,9 @@ sys.path.insert(0, str(ROOT))
 
 PEAK_F16_TFLOPS = 2500.0   # MI355X dense f16/bf16 MFMA (MI355X_MICROARCH.md chip table)
 PEAK_HBM_GBS = 8000.0      # HBM3E spec
+# Revision tag of the default prefill GEMM kernel; a PMC record's traffic is quoted only when its
+# config carries the same tag (r02-horner: the 256 x 256 Horner-form exact kernel).
+GEMM_REV = "r02-horner"
 
 
 def parse():
@@ -369,7 +372,7 @@ def main():
     flops_local = 2.0 * M * n_local * K
     abytes_local = algorithmic_bytes(M, K, n_local, args.bits, args.group)
     achieved_tflops = flops_local / (kernel_ms * 1e-3) / 1e12
-    pmc_cfg = {"M": M, "K": K, "N_local": n_local, "bits": args.bits, "group": args.group}
+    pmc_cfg = {"M": M, "K": K, "N_local": n_local, "bits": args.bits, "group": args.group, "rev": GEMM_REV}
     pmc = load_pmc_traffic(pmc_cfg)
     out = {
         "metric": "int4 dequant+GEMM GiB/s & tok/s per denoise step, 4096×4096, 1/2/4/8 GPU",

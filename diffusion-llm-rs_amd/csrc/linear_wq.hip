@@ -22,6 +22,11 @@
 #ifndef DLLM_LAB
 #define DLLM_LAB 0
 #endif
+// Horner-form exact GEMM: 1 = half of the reps are rescaled in the tail of the group's last stage
+// (the next group's ratios travel with that stage), half at the head of the group's first stage.
+#ifndef DLLM_HORNER_SPLIT
+#define DLLM_HORNER_SPLIT 0
+#endif
 
 #include <algorithm>
 #include <map>
@@ -42,6 +47,8 @@ struct dllm_linear {
     uint32_t *sz = nullptr;       // [G][Npad] f16 pairs {-(1024 + zp), f16(scale)}
     float *sf = nullptr;          // [G][Npad] f32 scales (exact-weight kernels; export), 0 in the padding
     float *bias = nullptr;        // [Npad]
+    float *hr = nullptr;          // [G + 1][Npad] Horner ratios s_{g-1} / s_g (built by the first 256 x 256-tile call)
+    int hstate = 0;               // Horner form: 0 not decided, 1 valid (hr built), 2 not valid for these scales
     __half *xws = nullptr;        // f32 -> f16 staging for X
     size_t xws_elems = 0;
     std::mutex mu;
@@ -321,6 +328,27 @@ __global__ void __launch_bounds__(256) build_sf_kernel(const float *__restrict__
     const size_t n = blockIdx.x * static_cast<size_t>(256) + threadIdx.x;
     const size_t g = blockIdx.y;
     if (n < Npad) sf[g * Npad + n] = n < N ? scales[g * N + n] : 0.0f;
+}
+
+// Horner ratios hr[g][n] = s_{g-1} / s_g (hr[0][n] = 1; padding columns 1) for the HORNER GEMM, and
+// *unsafe = 1 when some column's scales are not all finite normal f32 or span more than 2^64 (the
+// rescaled accumulator could overflow or lose its exponent range there).
+__global__ void __launch_bounds__(256) build_horner_kernel(const float *__restrict__ sf, size_t G, size_t N,
+                                                           size_t Npad, float *__restrict__ hr, int *__restrict__ unsafe) {
+    const size_t n = blockIdx.x * static_cast<size_t>(256) + threadIdx.x;
+    if (n >= Npad) return;
+    float mn = __builtin_inff(), mx = 0.0f, prev = 1.0f;
+    bool bad = false;
+    for (size_t g = 0; g < G; ++g) {
+        const float s = n < N ? sf[g * Npad + n] : 1.0f;
+        bad |= !(s >= 1.17549435e-38f && s <= 3.40282347e+38f);
+        mn = fminf(mn, s);
+        mx = fmaxf(mx, s);
+        hr[g * Npad + n] = g ? prev / s : 1.0f;
+        prev = s;
+    }
+    hr[G * Npad + n] = 1.0f;   // past the last group (read by the split schedule's last stage)
+    if (bad || mx > mn * 0x1p64f) atomicOr(unsafe, 1);
 }
 
 __global__ void __launch_bounds__(256) cast_f32_f16_kernel(const float *__restrict__ x, size_t n,
@@ -605,19 +633,33 @@ wq_gemm_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__res
 // 4/KG substeps kg*4/KG ..: KG = 2 puts two waves on each SIMD at the same tile count (the 128-row
 // tiles of mid-M shapes run one block per CU), their two accumulators summed through the stage
 // LDS at the end (fixed order).  SPLIT: as wq_gemm_kernel (slab partial, no bias).
+//
+// HORNER (exact weights, group 128, KG = 1, no K split): the MFMA A operand is the exact integer
+// q - zp (dequant_exact) and the f32 group scales enter in Horner form.  With r_g = s_{g-1} / s_g
+// (hr[g][n], f32; r_0 = 1) the accumulator is rescaled at the head of every group,
+//   acc <- acc * r_g + T_g   (T_g = the group's MFMA sum),
+// so after the last group G-1 acc = sum_g T_g s_g / s_{G-1}, and the epilogue multiplies by
+// s_{G-1} (sf).  Each term carries at most G f32 roundings of its ratio product (relative
+// <= G 2^-24).  There is no transient per-group accumulator (the fold form needs one beside acc),
+// so the 256 x 256 tile fits at two waves per SIMD.  Valid only where every scale is a finite
+// normal f32 and max_g s / min_g s <= 2^64 per column (build_horner_kernel decides per handle).
 template <int BITS, typename YT, int NW = 8, int MR = kMReps, bool SPLIT = false, int KG = 1, int LAB = 0,
-          int EPI = 0>
+          int EPI = 0, bool HORNER = false>
 __global__ void __launch_bounds__(NW * KG * 64, (NW * KG == 8 || MR == 8) ? 1 : 2)
 wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdev,
                 const uint32_t *__restrict__ sz, const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad,
                 int group, int nbm, int nbn, int nsplit = 1, float *__restrict__ ws = nullptr,
-                PSampleEpi epi = PSampleEpi{}) {
+                PSampleEpi epi = PSampleEpi{}, const float *__restrict__ hr = nullptr,
+                const float *__restrict__ sf = nullptr) {
     using SL = StageLayout8<BITS, NW, MR, KG>;
     constexpr int kBMt = 32 * MR, kBNt = 32 * NW, kWT = NW * KG, kSub = 4 / KG;
     static_assert(SL::kXRounds >= 1 && 4 * MR % kWT == 0, "X staging must split evenly over the waves");
-    __shared__ __attribute__((aligned(16))) uint8_t st0[SL::kBytes];
-    __shared__ __attribute__((aligned(16))) uint8_t st1[SL::kBytes];
-    __shared__ __attribute__((aligned(16))) uint8_t st2[SL::kBytes];
+    static_assert(!HORNER || (KG == 1 && !SPLIT && NW == 8 && LAB == 0), "Horner form: one k-group, whole K");
+    // HORNER: the group's ratios r_g (256 columns f32) follow the scale dwords in every stage.
+    constexpr int kHR = SL::kBytes, kStBytes = SL::kBytes + (HORNER ? 1024 : 0);
+    __shared__ __attribute__((aligned(16))) uint8_t st0[kStBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t st1[kStBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t st2[kStBytes];
 
     // K-slice outermost, so the blocks an XCD holds share the slice's X rows in its L2.
     const int nb = nbm * nbn * nsplit, orig = blockIdx.x;
@@ -652,15 +694,17 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
     // Scales: one 16-B LDS-DMA per block per k-step (wave szw; 4 columns per lane) instead of one
     // 256-B DMA per wave: each LDS-DMA costs its wave ~60-185 issue cycles whatever its size.
     const int szw = KG == 1 ? 0 : NW;
-    const bool has_w = KG == 1 || kg == 0, has_sz = wave == szw;
+    const bool has_w = KG == 1 || kg == 0, has_sz = wave == szw, has_hr = HORNER && wave == 1;
     const uint32_t *szsrc = sz + n0 + 4 * (lane & (8 * NW - 1));
+    const float *hrsrc = HORNER ? hr + n0 + 4 * lane : nullptr;
 
     const uint32_t wv = static_cast<uint32_t>(wave), cwv = static_cast<uint32_t>(cw);
     // A stage is kXRounds + 2 pieces: X rounds, the weight words, the scale dword (pieces a wave
     // does not own under KG = 2 are empty), issued as one burst at the top of a k-step.  Spreading
     // the pieces over the substeps (to hide each DMA's issue cost) measured slower: the later
-    // issue shortens the landing slack before the counted wait two steps on.
-    constexpr int kPieces = SL::kXRounds + 2;
+    // issue shortens the landing slack before the counted wait two steps on.  HORNER: + the
+    // group's ratios (wave 1).
+    constexpr int kPieces = SL::kXRounds + 2 + (HORNER ? 1 : 0);
     auto piece = [&](uint8_t *sb, unsigned kt, int p) {
         const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(sb));
         kt += kt0;
@@ -683,8 +727,11 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
                     glds4_asm(wp + 1, wb + 256);
                 }
             }
-        } else if (has_sz) {
-            glds16_asm(szsrc + (kt / kpg) * Npad, base + SL::kX + SL::kW);
+        } else if (p == SL::kXRounds + 1) {
+            if (has_sz) glds16_asm(szsrc + (kt / kpg) * Npad, base + SL::kX + SL::kW);
+        } else if (has_hr) {
+            // SPLIT: a group's second stage carries the NEXT group's ratios (row G = 1 after the last)
+            glds16_asm(hrsrc + (kt / kpg + (DLLM_HORNER_SPLIT ? (kt & 1) : 0)) * Npad, base + kHR);
         }
     };
     auto stage = [&](uint8_t *sb, unsigned kt) {
@@ -693,7 +740,7 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
     };
     // Counted wait leaving the newest stage's DMAs (this wave's own count) in flight.
     auto wait_prev = [&]() {
-        if (has_w && has_sz) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kXRounds + SL::kWOps + 1) : "memory");
+        if (has_w && (has_sz || has_hr)) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kXRounds + SL::kWOps + 1) : "memory");
         else if (has_w) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kXRounds + SL::kWOps) : "memory");
         else if (has_sz) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kXRounds + 1) : "memory");
         else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kXRounds) : "memory");
@@ -730,8 +777,9 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
 #pragma unroll
         for (int r = 0; r < MR; ++r) acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b[r], acc[r], 0, 0, 0);
     };
-    // Compute stage `sb`; stage `pf` receives k-step kt+2.
-    auto step = [&](const uint8_t *sb, uint8_t *pf, unsigned kt) {
+    // Compute stage `sb`; stage `pf` receives k-step kt+2.  gf_tag (HORNER): the stage opens a group.
+    auto step = [&](const uint8_t *sb, uint8_t *pf, unsigned kt, auto gf_tag) {
+        constexpr bool GF = HORNER && decltype(gf_tag)::value;
         const bool issue = kt + 2 < nk;
         if (!(LAB & 32) && issue) stage(pf, kt + 2);
         if constexpr (LAB & 4) {   // measurement only: the ring and its waits without any compute
@@ -751,26 +799,81 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
         }
         half2_t nz, sc;
         split_sz(*reinterpret_cast<const uint32_t *>(sb + SL::kX + SL::kW + (cw * 32 + (lane & 31)) * 4), nz, sc);
+        // HORNER: exact integer fragments; at a group's head the lane's 16 column ratios
+        // (columns 4 hsel + 8 qd + (0..3) of the wave's 32, as the accumulator registers).
+        ExactConsts ec;
+        float4 r4[4];
+        if constexpr (HORNER) ec = exact_consts(nz);
+        if constexpr (GF || (HORNER && DLLM_HORNER_SPLIT)) {
+            const float *rl = reinterpret_cast<const float *>(sb + kHR) + cw * 32 + 4 * hsel;
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd) r4[qd] = *reinterpret_cast<const float4 *>(rl + 8 * qd);
+        }
+        auto deq = [&](int j) {
+            if constexpr (HORNER) return dequant_exact<BITS>(w, j, ec);
+            else return dequant_frag<BITS>(w, j, nz, sc);
+        };
         half8_t bA[MR], bB[MR];
         read_b(bA, sb, 0);
         if constexpr (LAB & 32) {   // measurement: head-of-step LDS reads drained before the DMAs issue
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             if (issue) stage(pf, kt + 2);
         }
-        half8_t aA = dequant_frag<BITS>(w, 0, nz, sc), aB;
+        half8_t aA = deq(0), aB;
+        constexpr int kRH = (HORNER && DLLM_HORNER_SPLIT) ? MR / 2 : MR;   // reps rescaled at the group's head
+        auto rescale = [&](int r) {
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd) {
+                acc[r][4 * qd + 0] *= r4[qd].x;
+                acc[r][4 * qd + 1] *= r4[qd].y;
+                acc[r][4 * qd + 2] *= r4[qd].z;
+                acc[r][4 * qd + 3] *= r4[qd].w;
+            }
+        };
         auto sub = [&](half8_t (&bc)[MR], half8_t (&bn)[MR], const half8_t &ac, half8_t &an, int j) {
             __builtin_amdgcn_sched_barrier(0);
             __builtin_amdgcn_s_setprio(1);
             if (j < kSub - 1) {
                 read_b(bn, sb, j + 1);
-                an = dequant_frag<BITS>(w, j + 1, nz, sc);
+                an = deq(j + 1);
             }
-            mfma8(ac, bc);
+            if (GF && j == 0) {
+                // acc <- acc * r_g right before the group's first MFMA of each rep; scalar v_mul_f32
+                // (the file is built without the SLP vectorizer: v_pk_mul_f32 costs far more beside
+                // MFMAs, MI355X_MICROARCH.md filler prices)
 #pragma unroll
-            for (int i = 0; i < MR; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+                for (int r = 0; r < MR; ++r) {
+                    if (r < kRH) rescale(r);
+                    acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bc[r], acc[r], 0, 0, 0);
+                }
+                // rep i + 1's rescale issues beside rep i's MFMA (one rep of slack before its use)
+                __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
+#pragma unroll
+                for (int i = 0; i < MR; ++i) {
+                    if (i + 1 < kRH) __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);    // MFMA rep i
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, kRH < MR ? 2 : 1, 0);
+                }
+            } else if (HORNER && kRH < MR && !GF && j == kSub - 1) {
+                // the group's last substep: reps kRH.. take the next group's ratio after their last
+                // MFMA of this group (rep r's rescale beside rep r + 2's MFMA)
+                mfma8(ac, bc);
+#pragma unroll
+                for (int r = kRH; r < MR; ++r) rescale(r);
+#pragma unroll
+                for (int i = 0; i < MR; ++i) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    if (i >= kRH + 2) __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
+                }
+            } else {
+                mfma8(ac, bc);
+#pragma unroll
+                for (int i = 0; i < MR; ++i) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+                }
             }
             __builtin_amdgcn_s_setprio(0);
             __builtin_amdgcn_sched_barrier(0);
@@ -795,10 +898,37 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    for (unsigned kt = 0; kt < nk; kt += 3) {
-        step(st0, st2, kt);
-        if (kt + 1 < nk) step(st1, st0, kt + 1);
-        if (kt + 2 < nk) step(st2, st1, kt + 2);
+    using GFt = std::integral_constant<bool, true>;
+    using GFf = std::integral_constant<bool, false>;
+    if constexpr (HORNER) {
+        // group = 2 k-steps, ring period 3: unroll 6 so each step's buffer and group phase are static
+        for (unsigned kt = 0; kt < nk; kt += 6) {
+            step(st0, st2, kt, GFt{});
+            if (kt + 1 < nk) step(st1, st0, kt + 1, GFf{});
+            if (kt + 2 < nk) step(st2, st1, kt + 2, GFt{});
+            if (kt + 3 < nk) step(st0, st2, kt + 3, GFf{});
+            if (kt + 4 < nk) step(st1, st0, kt + 4, GFt{});
+            if (kt + 5 < nk) step(st2, st1, kt + 5, GFf{});
+        }
+        // acc = sum_g T_g s_g / s_{G-1}: times the last group's scales
+        const float *sl = sf + static_cast<size_t>(nk / 2 - 1) * Npad + n0 + cw * 32 + 4 * hsel;
+#pragma unroll
+        for (int qd = 0; qd < 4; ++qd) {
+            const float4 s = *reinterpret_cast<const float4 *>(sl + 8 * qd);
+#pragma unroll
+            for (int r = 0; r < MR; ++r) {
+                acc[r][4 * qd + 0] *= s.x;
+                acc[r][4 * qd + 1] *= s.y;
+                acc[r][4 * qd + 2] *= s.z;
+                acc[r][4 * qd + 3] *= s.w;
+            }
+        }
+    } else {
+        for (unsigned kt = 0; kt < nk; kt += 3) {
+            step(st0, st2, kt, GFf{});
+            if (kt + 1 < nk) step(st1, st0, kt + 1, GFf{});
+            if (kt + 2 < nk) step(st2, st1, kt + 2, GFf{});
+        }
     }
 
     if constexpr (KG == 2) {
@@ -1750,6 +1880,61 @@ int launch_rounded(const dllm_linear *h, const __half *X, int M, YT *Y, hipStrea
     return launch_ring<BITS, YT, 4, 4, 2, EPI>(h, X, M, Y, st, nsplit, epi);
 }
 
+// Exact-weight GEMM in Horner form (wq_gemm8_kernel<..., HORNER>, 256 x 256 tiles): for int4 g128
+// on grids of >= 256 such tiles.  The ratios and their validity are decided once per handle, by the
+// first such call outside stream capture (one synchronisation); a call inside a capture before that,
+// or a handle whose scales fail the check, runs the fold-form exact kernels.
+bool horner_ready(const dllm_linear *hc, int M, hipStream_t st) {
+    const int np = static_cast<int>(hc->Npad);
+    if (hc->precision != DLLM_PRECISION_EXACT || hc->bits != 4 || hc->group != 128 || hc->K % 128 != 0 ||
+        np % 256 != 0)
+        return false;
+    // rounds of 256 tiles: a 256 x 256 round takes about two 128 x 256 rounds, so the Horner grid
+    // must not need more rounds than half the fold form's (M = 4300: 2 vs 3 rounds -> fold form)
+    const int t256 = ((M + 255) / 256) * (np / 256), t128 = ((M + 127) / 128) * (np / 256);
+    if (t256 < kCUs || 2 * ((t256 + kCUs - 1) / kCUs) > (t128 + kCUs - 1) / kCUs) return false;
+#if DLLM_LAB
+    if (hc->variant == 14) return false;   // lab A/B: the fold-form exact policy
+#endif
+    dllm_linear *h = const_cast<dllm_linear *>(hc);
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (h->hstate) return h->hstate == 1;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(st, &cs);
+    if (cs != hipStreamCaptureStatusNone) return false;
+    float *hr = nullptr;
+    int *flag = nullptr, unsafe = 1;
+    if (hipMalloc(reinterpret_cast<void **>(&hr), (h->G + 1) * h->Npad * 4) != hipSuccess) return false;
+    if (hipMalloc(reinterpret_cast<void **>(&flag), sizeof(int)) != hipSuccess) { (void)hipFree(hr); return false; }
+    bool ok = hipMemsetAsync(flag, 0, sizeof(int), st) == hipSuccess;
+    if (ok) {
+        build_horner_kernel<<<static_cast<unsigned>((h->Npad + 255) / 256), 256, 0, st>>>(h->sf, h->G, h->N, h->Npad, hr, flag);
+        ok = hipGetLastError() == hipSuccess &&
+             hipMemcpyAsync(&unsafe, flag, sizeof(int), hipMemcpyDeviceToHost, st) == hipSuccess &&
+             hipStreamSynchronize(st) == hipSuccess;
+    }
+    (void)hipFree(flag);
+    if (!ok || unsafe) {
+        (void)hipFree(hr);
+        if (ok) h->hstate = 2;   // a failed build is retried by the next call
+        return false;
+    }
+    h->hr = hr;
+    h->hstate = 1;
+    return true;
+}
+
+template <typename YT, int EPI>
+int launch_horner(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t st, const PSampleEpi *epi) {
+    const int nbm = (M + 255) / 256, nbn = static_cast<int>(h->Npad / 256);
+    const PSampleEpi ep = epi ? *epi : PSampleEpi{};
+    wq_gemm8_kernel<4, YT, 8, 8, false, 1, 0, EPI, true><<<static_cast<unsigned>(nbm * nbn), 512, 0, st>>>(
+        X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn, 1, nullptr, ep,
+        h->hr, h->sf);
+    DLLM_LAUNCH_CHECK();
+    return DLLM_OK;
+}
+
 inline ExactGemmArgs exact_args(const dllm_linear *h, const __half *X, int M, void *Y, const PSampleEpi *epi) {
     ExactGemmArgs a{h->bits, X, M, (int)h->K, h->wdev, h->sz, h->sf, h->bias, Y, (int)h->N, (int)h->Npad,
                     (int)h->group, epi};
@@ -1774,7 +1959,10 @@ int launch_prefill_auto(const dllm_linear *h, const __half *X, int M, YT *Y, hip
         if (rc >= 0) return rc;
     }
 #endif
-    if (use_exact(h)) return launch_exact_gemm(exact_args(h, X, M, Y, epi), std::is_same<YT, float>::value ? 1 : 0, st);
+    if (use_exact(h)) {
+        if (BITS == 4 && horner_ready(h, M, st)) return launch_horner<YT, EPI>(h, X, M, Y, st, epi);
+        return launch_exact_gemm(exact_args(h, X, M, Y, epi), std::is_same<YT, float>::value ? 1 : 0, st);
+    }
     return launch_rounded<BITS, YT, EPI>(h, X, M, Y, st, epi);
 }
 
@@ -1798,7 +1986,7 @@ int launch_gemm(const dllm_linear *h, const __half *X, size_t M, void *Y, int y_
 void free_linear(dllm_linear *h) {
     if (!h) return;
     (void)hipFree(h->wdev); (void)hipFree(h->wdec); (void)hipFree(h->sz); (void)hipFree(h->sf);
-    (void)hipFree(h->bias); (void)hipFree(h->xws);
+    (void)hipFree(h->bias); (void)hipFree(h->xws); (void)hipFree(h->hr);
 #if DLLM_LAB
     (void)hipFree(h->w16);
 #endif
@@ -2075,6 +2263,7 @@ size_t dllm_linear_device_bytes(dllm_linear_t h) {
     if (!h) return 0;
     size_t b = h->Npad * h->K * h->bits / 8 + h->G * h->Npad * 8 + h->Npad * 4;   // wdev, sz + sf, bias
     if (h->wdec) b += h->Npad * ((h->K + 127) / 128) * 128 * h->bits / 8;          // decode layout, once built
+    if (h->hr) b += (h->G + 1) * h->Npad * 4;                                         // Horner ratios, once built
 #if DLLM_LAB
     b += h->Npad * h->K * h->bits / 8;
 #endif

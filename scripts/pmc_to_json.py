@@ -1,14 +1,17 @@
 """Per-launch HBM traffic of the bench GEMM kernel from rocprofv3 PMC passes (MI355X_MICROARCH.md
 HBM section: FETCH_SIZE reads 1/2 of a wide coalesced stream on gfx950 -> doubled, a factor this
 repo re-checks with scripts/pmc_calib.py; WRITE_SIZE is exact for 16-B stores; both in KiB).
-Usage: pmc_to_json.py <pmc root> <out.json> <kernel substring> [M K N_local bits group]; the config
-is recorded so bench.py only quotes the figure for the same shape."""
+Usage: pmc_to_json.py <pmc root> <out.json> <kernel substring> [M K N_local bits group [rev]]; the
+config (+ the kernel revision tag) is recorded so bench.py only quotes the figure for the same shape
+and the same kernel."""
 import csv, glob, json, statistics, sys
 root, out = sys.argv[1], sys.argv[2]
 regex = sys.argv[3] if len(sys.argv) > 3 else "wq_gemm8_kernel<4,"
 cfg = None
 if len(sys.argv) > 8:
     cfg = dict(zip(("M", "K", "N_local", "bits", "group"), (int(v) for v in sys.argv[4:9])))
+    if len(sys.argv) > 9:
+        cfg["rev"] = sys.argv[9]
 vals = {}
 for f in glob.glob(f"{root}/**/pmc_counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):

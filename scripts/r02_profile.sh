@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT="$PWD/gpurun_out/${PROF_OUT:-prof2}"
 mkdir -p "$OUT"
-KREGEX=${KREGEX:-wq_gemm_exact_kernel}
+KREGEX=${KREGEX:-wq_gemm8_kernel}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu --no-denoise > "$OUT/kt.log" 2>&1
 rc=$?; echo "kernel-trace rc=$rc"; tail -2 "$OUT/kt.log"
 [ $rc -eq 0 ] || exit $rc

@@ -476,6 +476,33 @@ def test_linear_exact_weights_tight(dllm, torch, orc, M, N, group):
     lin.close()
 
 
+@pytest.mark.parametrize("spread,M,K", [(8, 4096, 4096), (8, 4300, 1024), (30, 4096, 2048), (45, 4096, 1024)])
+def test_linear_horner_scale_spread(dllm, torch, orc, spread, M, K):
+    """The 256 x 256-tile exact kernel (int4 g128, >= 256 tiles) keeps one accumulator in Horner form:
+    acc <- acc * (s_{g-1} / s_g) + T_g, times s_{G-1} at the end.  Per-(group, column) weight
+    magnitudes spread by 2^U(-spread, spread): every column is checked on its own against f32 on the
+    same f16 X with the reference's a2 weights (quantization.rs:81-85), so a group rescaled wrongly
+    shows even where other groups dominate the column.  spread 45 gives columns whose scales span
+    more than 2^64: the handle must fall back to the fold-form kernel (same bound)."""
+    N = 4096
+    g = torch.Generator(device="cuda").manual_seed(spread + M + K)
+    G = K // 128
+    mult = torch.exp2((torch.rand(G, N, device="cuda", generator=g) * 2 - 1) * spread)
+    W = 0.02 * torch.randn(K, N, device="cuda", generator=g) * mult.repeat_interleave(128, 0)
+    X = torch.randn(M, K, device="cuda", generator=g).half()
+    lin = dllm.QuantLinear.from_weight(W, None, 4, 128)
+    codes, scales, zps = lin.export()
+    Wh = dev(torch, orc.dequantize_weights(orc.unpack_bits(host(codes), K * N, 4).reshape(K, N), host(scales),
+                                           host(zps), 128))
+    Yr = X.double() @ Wh.double()
+    for rep in range(2):   # the first call decides the Horner form, the second runs with it decided
+        Y = lin(X, out_dtype=torch.float32).double()
+        assert torch.isfinite(Y).all()
+        col = torch.linalg.norm(Y - Yr, dim=0) / torch.linalg.norm(Yr, dim=0)
+        assert col.max().item() <= EXACT_TOL, (spread, rep, col.max().item())
+    lin.close()
+
+
 @pytest.mark.parametrize("M,N,group", [(4096, 1024, 128), (4096, 512, 128), (1024, 4096, 128), (256, 4096, 256),
                                        (65, 4096, 128), (300, 1280, 64), (129, 384, 128)])
 def test_linear_split_k_combine_repeatable(dllm, torch, orc, M, N, group):
@@ -523,6 +550,12 @@ def test_linear_device_memory(dllm, torch):
     mib2 = lin.device_bytes() / 2**20
     assert 17.0 <= mib2 <= 17.05, mib2
     assert torch.equal(lin(X), y)
+    # the first call on a grid of >= 256 tiles of 256 x 256 adds the Horner ratios (f32 [G][N], 0.5 MiB)
+    Xp = torch.randn(4096, 4096, device="cuda").half()
+    y4 = lin(Xp)
+    mib3 = lin.device_bytes() / 2**20   # f16 X: no X workspace
+    assert 17.5 <= mib3 <= 17.55, mib3
+    assert torch.equal(lin(Xp), y4)
     lin.close()
 
 
