@@ -243,6 +243,7 @@ struct ExactGemmArgs {
     int N, Npad, group;
     const PSampleEpi *epi;
     int tm = 0;   // A/B: 256 x 256 tile-major tiles where they fill the chip
+    const float *hr = nullptr;   // Horner ratios (DLLM_EXACT_HORNER builds: the 128 x 256 tiles in Horner form)
 };
 int launch_exact_gemm(const ExactGemmArgs &a, int y_f32, hipStream_t st);
 bool exact_gemm_supported(int M, int K, int Npad, int group);

@@ -48,6 +48,11 @@
 #ifndef DLLM_EXACT_KG2
 #define DLLM_EXACT_KG2 1
 #endif
+// Horner form on the 128 x 256 tiles (A/B): one accumulator rescaled by s_{g-1}/s_g at each group
+// head instead of the transient group sum and its fold (see wq_gemm8_kernel<..., HORNER>).
+#ifndef DLLM_EXACT_HORNER
+#define DLLM_EXACT_HORNER 0
+#endif
 
 #include <algorithm>
 #include <type_traits>
@@ -86,13 +91,16 @@ struct ExactStage {
 // slice's stages (own LDS stage parts, same barriers); their sums are added in the epilogue,
 // k-group 0's first: a tile-starved grid gets two waves per SIMD without a second launch.
 template <int BITS, typename YT, int NW, int MR, int SPS, int KPG, bool SPLIT = false, int EPI = 0, bool TM = false,
-          int TMB = 1, bool WREG = false, int GPS = 1, int RING = 3, int KG = 1>
+          int TMB = 1, bool WREG = false, int GPS = 1, int RING = 3, int KG = 1, bool HORN = false>
 __global__ void __launch_bounds__(NW * KG * 64, NW * KG == 8 ? 1 : 2)
 wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdev,
                      const uint32_t *__restrict__ sz, const float *__restrict__ sf, const float *__restrict__ bias,
                      YT *__restrict__ Y, int N, int Npad, int group, int nbm, int nbn, int nsplit = 1,
-                     float *__restrict__ ws = nullptr, PSampleEpi epi = PSampleEpi{}) {
+                     float *__restrict__ ws = nullptr, PSampleEpi epi = PSampleEpi{},
+                     const float *__restrict__ sflast = nullptr) {
+    // HORN: `sf` is the Horner ratio array hr (staged where the scales were), `sflast` the scales
     using SL = ExactStage<BITS, NW, MR, SPS, WREG, GPS>;
+    static_assert(!HORN || (KPG == 1 && !TM && KG == 1 && !SPLIT && (GPS == 1 || RING == 2)), "Horner form: whole-group stages, whole K");
     static_assert(!WREG || (BITS == 4 && !TM), "register-staged weight words: int4, group-major stages");
     static_assert(GPS == 1 || (KPG == 1 && !TM && (4 * SPS) % GPS == 0 && 2 * GPS <= NW), "whole groups per stage");
     static_assert(RING == 3 || (RING == 2 && !TM), "ring depth");
@@ -253,7 +261,7 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
 #pragma unroll
             for (int qd = 0; qd < 4; ++qd) s4[qd] = *reinterpret_cast<const float4 *>(sfl + 8 * qd);
         };
-        if constexpr (GL && GPS == 1) read_s4(0);
+        if constexpr (HORN ? GF : (GL && GPS == 1)) read_s4(0);
         // acc[r] += s (.) T_g[r]
         auto fold = [&](int r) __attribute__((always_inline)) {
 #pragma unroll
@@ -271,8 +279,9 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
             constexpr bool glast = GPS > 1 ? v % kSubG == kSubG - 1 : (GL && v == kSub - 1);
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (DLLM_EXACT_PRIO) __builtin_amdgcn_s_setprio(1);
-            if constexpr (GPS > 1 && glast) read_s4(v / kSubG);
-            if constexpr (GPS > 1 && glast && v + 1 < kSub) {
+            if constexpr (!HORN && GPS > 1 && glast) read_s4(v / kSubG);
+            if constexpr (HORN && GPS > 1 && gfirst) read_s4(v / kSubG);   // this group's ratios
+            if constexpr (!HORN && GPS > 1 && glast && v + 1 < kSub) {
                 // A group's last substep with the next group's first in the same stage: prefetch the
                 // next fragments and fold this group beside its last MFMAs.
                 read_b(bn, sb, v + 1);
@@ -289,6 +298,45 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
                     __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);               // DS read
                     __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);               // dequant
                 }
+            } else if constexpr (HORN && v + 1 < kSub) {
+                read_b(bn, sb, v + 1);
+                an = dequant_exact<BITS>(w[(v + 1) / 4], (v + 1) % 4, ec[(v + 1) / kSubG]);
+                if constexpr (gfirst) {
+                    // acc <- acc * r_g before the group's first MFMA of each rep
+#pragma unroll
+                    for (int r = 0; r < MR; ++r) {
+#pragma unroll
+                        for (int qd = 0; qd < 4; ++qd) {
+                            acc[r][4 * qd + 0] *= s4[qd].x;
+                            acc[r][4 * qd + 1] *= s4[qd].y;
+                            acc[r][4 * qd + 2] *= s4[qd].z;
+                            acc[r][4 * qd + 3] *= s4[qd].w;
+                        }
+                        acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bc[r], acc[r], 0, 0, 0);
+                    }
+                    __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
+#pragma unroll
+                    for (int i = 0; i < MR; ++i) {
+                        if (i + 1 < MR) __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);   // rescale of rep i + 1
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < MR; ++r)
+                        acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bc[r], acc[r], 0, 0, 0);
+#pragma unroll
+                    for (int i = 0; i < MR; ++i) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+                    }
+                }
+            } else if constexpr (HORN) {
+#pragma unroll
+                for (int r = 0; r < MR; ++r)
+                    acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bc[r], acc[r], 0, 0, 0);
             } else if constexpr (v + 1 < kSub) {
                 read_b(bn, sb, v + 1);
                 an = dequant_exact<BITS>(w[(v + 1) / 4], (v + 1) % 4, ec[(v + 1) / kSubG]);
@@ -422,6 +470,21 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
         }(std::make_integer_sequence<int, kUnroll>{});
     }
 
+    if constexpr (HORN) {
+        // acc = sum_g T_g s_g / s_{G-1}: times the last group's scales
+        const float *sl = sflast + static_cast<size_t>(K / group - 1) * Npad + n0 + wave * 32 + 4 * hsel;
+#pragma unroll
+        for (int qd = 0; qd < 4; ++qd) {
+            const float4 sv = *reinterpret_cast<const float4 *>(sl + 8 * qd);
+#pragma unroll
+            for (int r = 0; r < MR; ++r) {
+                acc[r][4 * qd + 0] *= sv.x;
+                acc[r][4 * qd + 1] *= sv.y;
+                acc[r][4 * qd + 2] *= sv.z;
+                acc[r][4 * qd + 3] *= sv.w;
+            }
+        }
+    }
     if constexpr (KG == 2) {
         // k-group 1 hands its sums to k-group 0 through the (drained) ring: 16 B per lane per store.
         float4 *xch = reinterpret_cast<float4 *>(ring) + (wave * MR * 4) * 64 + lane;
@@ -501,8 +564,18 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
 }
 
 template <int BITS, typename YT, int NW, int MR, int SPS, int KPG, int EPI, bool TM = false, int GPS = 1, int RING = 3,
-          int KG = 1, bool WREG = (DLLM_EXACT_WREG != 0 && BITS == 4 && !TM)>
+          int KG = 1, bool WREG = (DLLM_EXACT_WREG != 0 && BITS == 4 && !TM), bool HORN = false>
 int launch_exact_tile(const ExactGemmArgs &a, int nsplit, hipStream_t st) {
+    if constexpr (HORN) {
+        const int nbm = (a.M + 32 * MR - 1) / (32 * MR), nbn = a.Npad / (32 * NW);
+        const PSampleEpi ep = a.epi ? *a.epi : PSampleEpi{};
+        wq_gemm_exact_kernel<BITS, YT, NW, MR, SPS, KPG, false, EPI, false, 1, WREG, GPS, RING, 1, true>
+            <<<static_cast<unsigned>(nbm * nbn), NW * 64, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.bias,
+                                                                    static_cast<YT *>(a.Y), a.N, a.Npad, a.group, nbm, nbn,
+                                                                    1, nullptr, ep, a.sf);
+        DLLM_LAUNCH_CHECK();
+        return DLLM_OK;
+    }
     const int nbm = (a.M + 32 * MR - 1) / (32 * MR), nbn = a.Npad / (32 * NW);
     const unsigned nb = static_cast<unsigned>(nbm * nbn * nsplit);
     const PSampleEpi ep = a.epi ? *a.epi : PSampleEpi{};
@@ -546,6 +619,14 @@ int launch_exact_bits(const ExactGemmArgs &a, hipStream_t st) {
         // two whole 128-row groups per stage, 2-stage ring: one barrier per two groups
         else if constexpr (G64 == 2 && BITS == 4 && DLLM_EXACT_WREG) return launch_exact_tile<BITS, YT, 8, 4, 4, 1, EPI, false, 2, 2>(a, 1, st);
 #endif
+        else if constexpr (G64 == 2 && BITS == 4 && DLLM_EXACT_HORNER) {
+#if DLLM_EXACT_HORNER == 2   // two groups per stage, 2-stage ring: one barrier per two groups
+            if (a.hr) return launch_exact_tile<BITS, YT, 8, 4, 4, 1, EPI, false, 2, 2, 1, DLLM_EXACT_WREG != 0, true>(a, 1, st);
+#else
+            if (a.hr) return launch_exact_tile<BITS, YT, 8, 4, 2, 1, EPI, false, 1, 3, 1, DLLM_EXACT_WREG != 0, true>(a, 1, st);
+#endif
+            return launch_exact_tile<BITS, YT, 8, 4, 2, 1, EPI>(a, 1, st);
+        }
         else return launch_exact_tile<BITS, YT, 8, 4, 2, G64 / 2, EPI>(a, 1, st);
     }
     const int tiles = mb * (a.Npad / 128), ngroups = a.K / a.group;

@@ -24,11 +24,15 @@
 #endif
 // Horner-form exact GEMM: 1 = half of the reps are rescaled in the tail of the group's last stage
 // (the next group's ratios travel with that stage), half at the head of the group's first stage.
+#ifndef DLLM_EXACT_HORNER
+#define DLLM_EXACT_HORNER 0
+#endif
 #ifndef DLLM_HORNER_SPLIT
 #define DLLM_HORNER_SPLIT 0
 #endif
 
 #include <algorithm>
+#include <cstdlib>
 #include <map>
 #include <tuple>
 #include <cstring>
@@ -1884,6 +1888,15 @@ int launch_rounded(const dllm_linear *h, const __half *X, int M, YT *Y, hipStrea
 // on grids of >= 256 such tiles.  The ratios and their validity are decided once per handle, by the
 // first such call outside stream capture (one synchronisation); a call inside a capture before that,
 // or a handle whose scales fail the check, runs the fold-form exact kernels.
+#if DLLM_LAB
+inline bool lab_horner128() {
+    static const bool on = std::getenv("DLLM_LAB_HORNER128") != nullptr;
+    return on;
+}
+#endif
+
+bool ensure_horner(const dllm_linear *hc, hipStream_t st);
+
 bool horner_ready(const dllm_linear *hc, int M, hipStream_t st) {
     const int np = static_cast<int>(hc->Npad);
     if (hc->precision != DLLM_PRECISION_EXACT || hc->bits != 4 || hc->group != 128 || hc->K % 128 != 0 ||
@@ -1892,10 +1905,21 @@ bool horner_ready(const dllm_linear *hc, int M, hipStream_t st) {
     // rounds of 256 tiles: a 256 x 256 round takes about two 128 x 256 rounds, so the Horner grid
     // must not need more rounds than half the fold form's (M = 4300: 2 vs 3 rounds -> fold form)
     const int t256 = ((M + 255) / 256) * (np / 256), t128 = ((M + 127) / 128) * (np / 256);
-    if (t256 < kCUs || 2 * ((t256 + kCUs - 1) / kCUs) > (t128 + kCUs - 1) / kCUs) return false;
 #if DLLM_LAB
     if (hc->variant == 14) return false;   // lab A/B: the fold-form exact policy
+    if (lab_horner128()) {                 // lab A/B: Horner form on 128 x 256 tiles
+        if (t128 < kCUs) return false;
+    } else
 #endif
+    if (t256 < kCUs || 2 * ((t256 + kCUs - 1) / kCUs) > (t128 + kCUs - 1) / kCUs) return false;
+    return ensure_horner(hc, st);
+}
+
+// Builds the handle's Horner ratios and decides their validity, once (see horner_ready).
+bool ensure_horner(const dllm_linear *hc, hipStream_t st) {
+    if (hc->precision != DLLM_PRECISION_EXACT || hc->bits != 4 || hc->group != 128 || hc->K % 128 != 0 ||
+        hc->Npad % 256 != 0)
+        return false;
     dllm_linear *h = const_cast<dllm_linear *>(hc);
     std::lock_guard<std::mutex> lk(h->mu);
     if (h->hstate) return h->hstate == 1;
@@ -1926,8 +1950,18 @@ bool horner_ready(const dllm_linear *hc, int M, hipStream_t st) {
 
 template <typename YT, int EPI>
 int launch_horner(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t st, const PSampleEpi *epi) {
-    const int nbm = (M + 255) / 256, nbn = static_cast<int>(h->Npad / 256);
     const PSampleEpi ep = epi ? *epi : PSampleEpi{};
+#if DLLM_LAB
+    if (lab_horner128()) {
+        const int nbm = (M + 127) / 128, nbn = static_cast<int>(h->Npad / 256);
+        wq_gemm8_kernel<4, YT, 8, 4, false, 1, 0, EPI, true><<<static_cast<unsigned>(nbm * nbn), 512, 0, st>>>(
+            X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn, 1, nullptr,
+            ep, h->hr, h->sf);
+        DLLM_LAUNCH_CHECK();
+        return DLLM_OK;
+    }
+#endif
+    const int nbm = (M + 255) / 256, nbn = static_cast<int>(h->Npad / 256);
     wq_gemm8_kernel<4, YT, 8, 8, false, 1, 0, EPI, true><<<static_cast<unsigned>(nbm * nbn), 512, 0, st>>>(
         X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn, 1, nullptr, ep,
         h->hr, h->sf);
@@ -1961,7 +1995,11 @@ int launch_prefill_auto(const dllm_linear *h, const __half *X, int M, YT *Y, hip
 #endif
     if (use_exact(h)) {
         if (BITS == 4 && horner_ready(h, M, st)) return launch_horner<YT, EPI>(h, X, M, Y, st, epi);
-        return launch_exact_gemm(exact_args(h, X, M, Y, epi), std::is_same<YT, float>::value ? 1 : 0, st);
+        ExactGemmArgs a = exact_args(h, X, M, Y, epi);
+#if DLLM_EXACT_HORNER   // A/B build: the 128 x 256 exact tiles in Horner form too
+        if (BITS == 4 && ensure_horner(h, st)) a.hr = h->hr;
+#endif
+        return launch_exact_gemm(a, std::is_same<YT, float>::value ? 1 : 0, st);
     }
     return launch_rounded<BITS, YT, EPI>(h, X, M, Y, st, epi);
 }
