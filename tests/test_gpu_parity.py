@@ -587,6 +587,42 @@ def test_linear_decode_layout_refused_in_capture(dllm, torch):
     ref.close()
 
 
+def test_linear_horner_first_call_in_capture(dllm, torch, orc):
+    """A handle's first call on a Horner grid (M = K = N = 4096, int4 g128) decides the Horner form
+    with one synchronisation; inside stream capture it must not, so the captured call runs the
+    fold-form exact kernel (no allocation, no sync recorded) and replays correctly, and the first
+    eager call afterwards builds the ratios (+0.52 MiB) and runs the Horner kernel -- both within
+    the exact-weights bound of f32 on the same f16 X."""
+    K = N = M = 4096
+    g = torch.Generator(device="cuda").manual_seed(4242)
+    W = 0.02 * torch.randn(K, N, device="cuda", generator=g)
+    X = torch.randn(M, K, device="cuda", generator=g).half()
+    lin = dllm.QuantLinear.from_weight(W, None, 4, 128)
+    codes, scales, zps = lin.export()
+    Wh = dev(torch, orc.dequantize_weights(orc.unpack_bits(host(codes), K * N, 4).reshape(K, N), host(scales),
+                                           host(zps), 128))
+    Yr = X.float() @ Wh
+    Yg = torch.empty(M, N, device="cuda")
+    before = lin.device_bytes()
+    s = torch.cuda.Stream()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(graph, stream=s):
+            lin(X, out=Yg)
+    graph.replay()
+    torch.cuda.synchronize()
+    assert lin.device_bytes() == before, "no Horner ratios may be built inside capture"
+    rel_g = (torch.linalg.norm(Yg - Yr) / torch.linalg.norm(Yr)).item()
+    Ye = lin(X, out_dtype=torch.float32)
+    assert lin.device_bytes() == before + 33 * 4096 * 4
+    rel_e = (torch.linalg.norm(Ye - Yr) / torch.linalg.norm(Yr)).item()
+    assert rel_g <= EXACT_TOL and rel_e <= EXACT_TOL, (rel_g, rel_e)
+    graph.replay()                    # the graph keeps its fold-form kernel
+    torch.cuda.synchronize()
+    assert rel_g == (torch.linalg.norm(Yg - Yr) / torch.linalg.norm(Yr)).item()
+    lin.close()
+
+
 @pytest.mark.lab
 @pytest.mark.parametrize("variant", [4, 8, 9, 10, 11, 14, 15])
 @pytest.mark.parametrize("bits", [2, 4, 8])
