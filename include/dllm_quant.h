@@ -214,7 +214,11 @@ int dllm_linear_create_quantized_ex(const uint8_t *packed_codes, const float *sc
  * order (deterministic) through a per-(device, stream) workspace.  Both workspaces only grow and
  * are allocated on the first call that needs them, which therefore must precede stream capture;
  * likewise the decode-fragment copy of the weights, built by the handle's first M <= 64 call
- * (a capture-time first call returns DLLM_ERR_INVALID_PARAMS). */
+ * (a capture-time first call returns DLLM_ERR_INVALID_PARAMS).  DLLM_PRECISION_EXACT, int4 g128,
+ * on grids of >= 256 tiles of 256 x 256 (M >= 4096 at N = 4096): the handle's first such call
+ * builds the Horner-form ratios s_{g-1}/s_g (one synchronisation, [G + 1][N] f32) and checks that
+ * the scales allow that form; inside stream capture it does not, and the call runs the fold-form
+ * kernel instead (same bound, different f32 summation order). */
 int dllm_linear_forward(dllm_linear_t h, const void *X, size_t M, int x_dtype, void *Y, int y_dtype,
                         dllm_stream_t stream);
 /* Export the quantized weights in canonical form (packed bitstream [K][N], scales [G][N], zps);
@@ -227,7 +231,8 @@ int dllm_linear_precision(dllm_linear_t h);   /* DLLM_PRECISION_*, -1 on a null 
 size_t dllm_linear_weight_bytes(dllm_linear_t h);
 /* Device memory the handle owns: the prefill code layout and the per-(group, column) parameters
  * (f16 zero-point/scale pairs + f32 scales) -- 9.02 MiB at 4096 x 4096 int4 g128 -- plus, once
- * built, the decode code layout (+8 MiB there) and the X staging workspace once grown. */
+ * built, the decode code layout (+8 MiB there), the Horner ratios (+0.52 MiB there) and the X
+ * staging workspace once grown. */
 size_t dllm_linear_device_bytes(dllm_linear_t h);
 #ifdef DLLM_LAB
 /* Lab build only (libdllm_hip_lab.so): A/B schedule variants and ablation masks; mutates the
