@@ -30,6 +30,13 @@
 #ifndef DLLM_HORNER_SPLIT
 #define DLLM_HORNER_SPLIT 0
 #endif
+// Horner form: 1 = the ratios travel only with a group's first stage (one LDS-DMA per two stages).
+#ifndef DLLM_HORNER_HR_GF
+#define DLLM_HORNER_HR_GF 0
+#endif
+#if DLLM_HORNER_HR_GF && DLLM_HORNER_SPLIT
+#error "DLLM_HORNER_SPLIT reads the next group's ratios in every group's second stage"
+#endif
 
 #include <algorithm>
 #include <cstdlib>
@@ -709,7 +716,7 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
     // issue shortens the landing slack before the counted wait two steps on.  HORNER: + the
     // group's ratios (wave 1).
     constexpr int kPieces = SL::kXRounds + 2 + (HORNER ? 1 : 0);
-    auto piece = [&](uint8_t *sb, unsigned kt, int p) {
+    auto piece = [&](uint8_t *sb, unsigned kt, int p, bool with_hr) {
         const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(sb));
         kt += kt0;
         if (p < SL::kXRounds) {
@@ -733,18 +740,19 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
             }
         } else if (p == SL::kXRounds + 1) {
             if (has_sz) glds16_asm(szsrc + (kt / kpg) * Npad, base + SL::kX + SL::kW);
-        } else if (has_hr) {
+        } else if (has_hr && with_hr) {
             // SPLIT: a group's second stage carries the NEXT group's ratios (row G = 1 after the last)
             glds16_asm(hrsrc + (kt / kpg + (DLLM_HORNER_SPLIT ? (kt & 1) : 0)) * Npad, base + kHR);
         }
     };
-    auto stage = [&](uint8_t *sb, unsigned kt) {
+    // with_hr (DLLM_HORNER_HR_GF): the stage opens a group, so its ratios travel with it
+    auto stage = [&](uint8_t *sb, unsigned kt, bool with_hr = true) {
 #pragma unroll
-        for (int p = 0; p < kPieces; ++p) piece(sb, kt, p);
+        for (int p = 0; p < kPieces; ++p) piece(sb, kt, p, with_hr);
     };
     // Counted wait leaving the newest stage's DMAs (this wave's own count) in flight.
-    auto wait_prev = [&]() {
-        if (has_w && (has_sz || has_hr)) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kXRounds + SL::kWOps + 1) : "memory");
+    auto wait_prev = [&](bool newest_hr = true) {
+        if (has_w && (has_sz || (has_hr && newest_hr))) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kXRounds + SL::kWOps + 1) : "memory");
         else if (has_w) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kXRounds + SL::kWOps) : "memory");
         else if (has_sz) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kXRounds + 1) : "memory");
         else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kXRounds) : "memory");
@@ -785,7 +793,7 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
     auto step = [&](const uint8_t *sb, uint8_t *pf, unsigned kt, auto gf_tag) {
         constexpr bool GF = HORNER && decltype(gf_tag)::value;
         const bool issue = kt + 2 < nk;
-        if (!(LAB & 32) && issue) stage(pf, kt + 2);
+        if (!(LAB & 32) && issue) stage(pf, kt + 2, !DLLM_HORNER_HR_GF || GF);   // kt + 2 has kt's group phase
         if constexpr (LAB & 4) {   // measurement only: the ring and its waits without any compute
             if (issue) wait_prev();
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -889,7 +897,7 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
             sub(bB, bA, aB, aA, 3);
         }
         // Stage kt+1 must have landed; kt+2's DMAs may stay in flight across the barrier.
-        if (issue && !(LAB & 16)) wait_prev();
+        if (issue && !(LAB & 16)) wait_prev(!DLLM_HORNER_HR_GF || GF);
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
@@ -897,8 +905,8 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
     };
 
     stage(st0, 0);
-    if (nk > 1) stage(st1, 1);
-    if (nk > 1) wait_prev();
+    if (nk > 1) stage(st1, 1, !DLLM_HORNER_HR_GF || !HORNER);
+    if (nk > 1) wait_prev(!DLLM_HORNER_HR_GF || !HORNER);
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
