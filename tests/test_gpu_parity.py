@@ -476,7 +476,7 @@ def test_linear_exact_weights_tight(dllm, torch, orc, M, N, group):
     lin.close()
 
 
-@pytest.mark.parametrize("spread,M,K", [(8, 4096, 4096), (8, 4300, 1024), (30, 4096, 2048), (45, 4096, 1024)])
+@pytest.mark.parametrize("spread,M,K", [(8, 4096, 4096), (8, 8000, 1024), (8, 4300, 1024), (30, 4096, 2048), (45, 4096, 1024)])
 def test_linear_horner_scale_spread(dllm, torch, orc, spread, M, K):
     """The 256 x 256-tile exact kernel (int4 g128, >= 256 tiles) keeps one accumulator in Horner form:
     acc <- acc * (s_{g-1} / s_g) + T_g, times s_{G-1} at the end.  Per-(group, column) weight
