@@ -215,20 +215,37 @@ class _ComputeOnlyPair:
 
 
 def denoise_loop_tp(d, torch, dist, dev, world, steps):
-    """Config C5 hidden-dim sharded over the job's ranks: 12 int4 layers as 6
-    Megatron pairs (parallel.TensorParallelPair: column shard, row shard, one reduction of the f32
-    partial [2048, 4096] per pair over RCCL), p_sample after the last pair, no KV cache.  Every
-    rank builds the same full weights (seeded) and keeps its shard.  Each reduction mode is timed
-    with a barrier and synchronize on both sides, max over ranks: "allreduce" (f32 all_reduce, then
-    bias + f16 cast) and "rs_ag" (f32 reduce_scatter over token rows, cast on the local rows, f16
-    all_gather: 3/4 of the bytes), each unchunked and with the reduction split into 4 token chunks
-    that overlap the next chunk's GEMM.  "compute_only": the same loop with each pair's reduction
-    left out (the GEMMs, casts and p_sample only)."""
+    """Config C5 hidden-dim sharded over the job's ranks, the same work per step as
+    ``denoise_loop``: 12 int4 layers as 6 Megatron pairs (parallel.TensorParallelPair: column shard,
+    row shard, one reduction of the f32 partial [2048, 4096] per pair over RCCL), p_sample after the
+    last pair, and the KV step of every timestep on the head-sharded phase-aware cache
+    (parallel.HeadParallelKVCacheEntry: the rank's 32/N heads of K, V [1, 2048, 4096]; phase switch,
+    progressive decode widths, one all_reduce(MAX) of 4 floats per update, both widths from it).
+    Every rank builds the same full weights and K/V (seeded) and keeps its shard.  Each reduction
+    mode is timed with a barrier and synchronize on both sides, max over ranks: "allreduce" (f32
+    all_reduce, then bias + f16 cast) and "rs_ag" (f32 reduce_scatter over token rows, cast on the
+    local rows, f16 all_gather: 3/4 of the bytes), each unchunked and with the reduction split into 4
+    token chunks that overlap the next chunk's GEMM.  "compute_only": the same loop with each pair's
+    reduction left out (the GEMMs, casts, KV step and p_sample only).  Serial schedule (the KV step
+    and its 4-float all-reduce in stream order before the layers)."""
     par = d.parallel
-    dm, M, L = 4096, 2048, 12
+    dm, M, L, heads = 4096, 2048, 12, 32
+    rank = dist.get_rank()
+    c0, c1 = par.head_columns(dm, heads, world, rank)
     res = {"workload": f"C5 hidden-dim sharded: {L // 2} TensorParallelPair of int4-g128 d{dm}, seq {M}, "
-                       f"{steps} steps, one reduction of the f32 [{M}, {dm}] partial per pair, p_sample, no KV cache",
+                       f"{steps} steps, one reduction of the f32 [{M}, {dm}] partial per pair, p_sample, KV step on "
+                       f"the head-sharded phase-aware cache ({heads // world} of {heads} heads per rank)",
            "n_ranks": world}
+
+    def kv_cache(cfg):
+        gk = torch.Generator(device=dev).manual_seed(98)
+        K = torch.randn(1, M, dm, device=dev, generator=gk)
+        V = torch.randn(1, M, dm, device=dev, generator=gk)
+        kv = par.HeadParallelKVCacheEntry(K[..., c0:c1].contiguous(), V[..., c0:c1].contiguous(), cfg.prefill_bits,
+                                          cfg.decode_bits)
+        del K, V
+        return kv
+
     for mode in ("allreduce", "rs_ag"):
         g = torch.Generator(device=dev).manual_seed(99)
         pairs = []
@@ -237,12 +254,13 @@ def denoise_loop_tp(d, torch, dist, dev, world, steps):
             WB = (0.5 / 64.0) * torch.randn(dm, dm, device=dev, generator=g)
             pairs.append(par.TensorParallelPair(WA, None, WB, None, 4, 128, reduce=mode))
             del WA, WB
-        cfg = d.DiffusionConfig(num_timesteps=steps, hidden_size=dm, num_layers=L)
-        loop = d.DenoiseLoop(pairs, cfg, cumprod=d.Cumprod.INCLUSIVE, seed=1, kv_cache=None, overlap=False)
+        cfg = d.DiffusionConfig(num_timesteps=steps, hidden_size=dm, num_layers=L, num_attention_heads=heads)
         x = torch.randn(M, dm, device=dev, generator=g)
         for chunks in (1, 4):   # 4: each pair's reduction issued per token chunk, overlapping the next GEMM
             for p in pairs:
                 p.chunks = chunks
+            loop = d.DenoiseLoop(pairs, cfg, cumprod=d.Cumprod.INCLUSIVE, seed=1, kv_cache=kv_cache(cfg),
+                                 overlap=False)
             loop.sample(x, 2)
             torch.cuda.synchronize()
             dist.barrier()
@@ -258,7 +276,7 @@ def denoise_loop_tp(d, torch, dist, dev, world, steps):
                         "finite": bool(torch.isfinite(out).all())}
         if mode == "allreduce":
             loop_c = d.DenoiseLoop([_ComputeOnlyPair(p) for p in pairs], cfg, cumprod=d.Cumprod.INCLUSIVE, seed=1,
-                                   kv_cache=None, overlap=False)
+                                   kv_cache=kv_cache(cfg), overlap=False)
             loop_c.sample(x, 2)
             torch.cuda.synchronize()
             dist.barrier()
@@ -271,7 +289,8 @@ def denoise_loop_tp(d, torch, dist, dev, world, steps):
             s = float(t.item())
             res["compute_only"] = {"ms_per_step": round(s / steps * 1e3, 4),
                                    "tok_per_s_per_step": round(M / (s / steps), 1),
-                                   "note": "the pairs' local GEMMs + casts + p_sample, no reduction (timing only)"}
+                                   "note": "the pairs' local GEMMs + casts + KV step + p_sample, no pair reduction "
+                                           "(timing only)"}
         for p in pairs:
             p.close()
     return res

@@ -92,6 +92,7 @@ SIGNATURES = {
     "dllm_tensor_extremes": (INT, [P, S, P, P, S, P]),
     "dllm_quantize_params_from_extremes": (INT, [P, U8, P, P]),
     "dllm_quantize_tensor_with_params": (INT, [P, S, U8, INT, P, P, P]),
+    "dllm_quantize_tensor_pair_with_params": (INT, [P, S, U8, U8, INT, P, P, P, P, P]),
     "dllm_adaptive_update": (INT, [P, S, P, P, S, P]),
     "dllm_adaptive_compute_params": (INT, [P, INT, U32, P, P]),
     "dllm_adaptive_quantize": (INT, [P, S, U32, P, INT, P, P]),
@@ -140,6 +141,7 @@ SIGNATURES = {
     "dllm_compressed_vector_to_bincode": (INT, [P, S, P, S, U8, P, S, FL, FL, P, S, P]),
     "dllm_compressed_vector_from_bincode": (INT, [P, S, INT, P, S, P, P, S, P, P, P, S, P, P, P]),
     "dllm_compressed_vector_to_json": (INT, [P, S, P, S, U8, P, S, FL, FL, P, S, P]),
+    "dllm_compressed_vector_from_json": (INT, [P, S, P, S, P, P, S, P, P, P, S, P, P, P]),
     "dllm_linear_forward_host": (INT, [P, P, S, P]),
 }
 

@@ -28,6 +28,10 @@
 // kernel (measured by ablation: DLLM_ATTN_LAB=2).
 #include "common.hpp"
 
+#ifndef DLLM_LAB
+#define DLLM_LAB 0
+#endif
+
 #include <cstdlib>
 
 typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
@@ -180,6 +184,7 @@ __global__ void __launch_bounds__(512) kv_stage_kernel(const uint8_t *__restrict
     for (int i = tid; i < kVImg / 16; i += 512) reinterpret_cast<uint4 *>(dst + kKImg)[i] = sv[i];
 }
 
+#if DLLM_LAB   // lab build only: v4, the unscheduled form of v5 (A/B and ablation masks)
 template <int LAB = 0>
 __global__ void __launch_bounds__(kWaves * 64)
 kv_attention_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__ img, const float *__restrict__ kp,
@@ -371,7 +376,7 @@ kv_attention_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__ 
         }
     }
 }
-
+#endif  // DLLM_LAB
 
 // Row reductions across the two lane halves (lane l and l ^ 32 hold the two key halves of one
 // query): v_permlane32_swap (VALU) instead of a ds_bpermute round trip through the LDS unit.
@@ -647,6 +652,7 @@ kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__
 }
 
 
+#if DLLM_LAB   // lab build only: v6, A/B against v5 (bit-identical, slower: DESIGN.md section 4)
 // v6: one wave per SIMD (4 waves per workgroup, the same 256 queries and LDS ring), each wave
 // owning 64 queries as two 32-query blocks b = 0, 1 with the whole 512-entry register file
 // (__launch_bounds__(256, 1)).  Every K fragment read from LDS feeds the S^T MFMAs of both query
@@ -892,6 +898,7 @@ kv_attention6_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__
         }
 }
 
+#endif  // DLLM_LAB
 }  // namespace
 }  // namespace dllm
 
@@ -920,14 +927,15 @@ extern "C" int dllm_kv_attention(const void *Q, const uint8_t *Kq, const float *
         kv_stage_kernel<8><<<sgrid, 512, 0, st>>>(Kq, k_params, Vq, v_params, (int)S, (int)H, nkb, img);
     DLLM_LAUNCH_CHECK();
     dim3 grid(static_cast<unsigned>((S + kQT - 1) / kQT), static_cast<unsigned>(H));
-    // DLLM_ATTN_LAB (measurement only; results are garbage when set): 1 no softmax, 2 no K/V
-    // staging, 4 no PV MFMAs, 8 no QK MFMAs (on the v4 kernel); 100: the v4 kernel itself (valid
-    // results); 100 + mask: the same masks on the v5 kernel, plus 16 no vmcnt wait at the end of a
-    // k-block, 32 no barrier there, 64 register staging instead of LDS-DMA (valid results).
-    // read per call (a getenv, ~0.1 us) so that a test can A/B the schedules in one process
-    const int lab = [] { const char *e = getenv("DLLM_ATTN_LAB"); return e ? atoi(e) : 0; }();
     const _Float16 *Qh = static_cast<const _Float16 *>(Q);
     _Float16 *Oh = static_cast<_Float16 *>(O);
+#if DLLM_LAB
+    // DLLM_ATTN_LAB (lab build only, measurement; results are garbage when set): 1 no softmax, 2 no
+    // K/V staging, 4 no PV MFMAs, 8 no QK MFMAs (on the v4 kernel); 100: the v4 kernel itself
+    // (valid results); 100 + mask: the same masks on the v5 kernel, plus 16 no vmcnt wait at the
+    // end of a k-block, 32 no barrier there, 64 register staging instead of LDS-DMA (valid
+    // results); 200 (+ mask): v6.  Read per call so that a script can A/B the schedules in one process.
+    const int lab = [] { const char *e = getenv("DLLM_ATTN_LAB"); return e ? atoi(e) : 0; }();
     switch (lab) {
 #define DLLM_ALAB(L) case L: kv_attention_kernel<L><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh); break;
         DLLM_ALAB(1) DLLM_ALAB(2) DLLM_ALAB(3) DLLM_ALAB(4) DLLM_ALAB(5) DLLM_ALAB(6) DLLM_ALAB(7)
@@ -950,6 +958,9 @@ extern "C" int dllm_kv_attention(const void *Q, const uint8_t *Kq, const float *
             kv_attention5_kernel<0><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh);
             break;
     }
+#else
+    kv_attention5_kernel<0><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh);
+#endif
     DLLM_LAUNCH_CHECK();
     return DLLM_OK;
 }

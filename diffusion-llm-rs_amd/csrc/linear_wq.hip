@@ -54,12 +54,12 @@ struct dllm_linear {
     int device = 0;
     int precision = DLLM_PRECISION_EXACT;
     uint32_t *wdev = nullptr;     // prefill layout (32x32x16 fragments)
-    uint32_t *wdec = nullptr;     // decode layout (16x16x32 fragments), built by the first M <= 64 call
+    uint32_t *wdec = nullptr;     // decode layout (16x16x32 fragments)
     uint32_t *sz = nullptr;       // [G][Npad] f16 pairs {-(1024 + zp), f16(scale)}
     float *sf = nullptr;          // [G][Npad] f32 scales (exact-weight kernels; export), 0 in the padding
     float *bias = nullptr;        // [Npad]
-    float *hr = nullptr;          // [G + 1][Npad] Horner ratios s_{g-1} / s_g (built by the first 256 x 256-tile call)
-    int hstate = 0;               // Horner form: 0 not decided, 1 valid (hr built), 2 not valid for these scales
+    float *hr = nullptr;          // [G + 1][Npad] Horner ratios s_{g-1} / s_g (Horner-form shapes with valid scales)
+    int hstate = 0;               // Horner form: 0 not applicable, 1 valid (hr kept), 2 not valid for these scales
     __half *xws = nullptr;        // f32 -> f16 staging for X
     size_t xws_elems = 0;
     std::mutex mu;
@@ -1705,23 +1705,10 @@ int launch_decode_lab(const dllm_linear *h, const __half *X, size_t M, YT *Y, hi
 }
 #endif
 
-// The decode layout is built on the first decode-shaped call (prefill-only layers never hold it);
-// that call must precede stream capture, like the workspaces.
-int ensure_decode_layout(const dllm_linear *hc, hipStream_t st) {
-    dllm_linear *h = const_cast<dllm_linear *>(hc);
-    std::lock_guard<std::mutex> lk(h->mu);
-    if (h->wdec) return DLLM_OK;
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    (void)hipStreamIsCapturing(st, &cs);
-    if (cs != hipStreamCaptureStatusNone)
-        return fail(DLLM_ERR_INVALID_PARAMS, "the decode layout is built by the first M <= 64 call: run one before stream capture");
-    uint32_t *w = nullptr;
-    DLLM_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&w), h->Npad * ((h->K + 127) / 128) * 128 * h->bits / 8));
-    dim3 gd(static_cast<unsigned>((h->Npad + 255) / 256), static_cast<unsigned>((h->K + 127) / 128));
-    build_decode_from_wdev_kernel<<<gd, 256, 0, st>>>(h->wdev, h->K, h->Npad, h->bits, w);
-    if (hipGetLastError() != hipSuccess) { (void)hipFree(w); return fail(DLLM_ERR_HIP, "decode layout build launch"); }
-    h->wdec = w;
-    return DLLM_OK;
+// Both code layouts are built by the handle's create (finish_linear), so a forward call never
+// allocates, builds or synchronises, and behaves the same inside and outside stream capture.
+int ensure_decode_layout(const dllm_linear *h, hipStream_t) {
+    return h->wdec ? DLLM_OK : fail(DLLM_ERR_INVALID_PARAMS, "linear handle has no decode layout");
 }
 
 template <int BITS, typename YT>
@@ -1893,9 +1880,8 @@ int launch_rounded(const dllm_linear *h, const __half *X, int M, YT *Y, hipStrea
 }
 
 // Exact-weight GEMM in Horner form (wq_gemm8_kernel<..., HORNER>, 256 x 256 tiles): for int4 g128
-// on grids of >= 256 such tiles.  The ratios and their validity are decided once per handle, by the
-// first such call outside stream capture (one synchronisation); a call inside a capture before that,
-// or a handle whose scales fail the check, runs the fold-form exact kernels.
+// on grids of >= 256 such tiles.  The ratios and their validity are decided once, by the handle's
+// create (finish_linear); a handle whose scales fail the check runs the fold-form exact kernels.
 #if DLLM_LAB
 inline bool lab_horner128() {
     static const bool on = std::getenv("DLLM_LAB_HORNER128") != nullptr;
@@ -1903,13 +1889,17 @@ inline bool lab_horner128() {
 }
 #endif
 
-bool ensure_horner(const dllm_linear *hc, hipStream_t st);
+inline bool horner_shape(const dllm_linear *h) {
+    return h->precision == DLLM_PRECISION_EXACT && h->bits == 4 && h->group == 128 && h->K % 128 == 0 &&
+           h->Npad % 256 == 0;
+}
+
+// The handle's Horner ratios are valid (decided at create, immutable afterwards).
+inline bool ensure_horner(const dllm_linear *h, hipStream_t) { return h->hstate == 1; }
 
 bool horner_ready(const dllm_linear *hc, int M, hipStream_t st) {
     const int np = static_cast<int>(hc->Npad);
-    if (hc->precision != DLLM_PRECISION_EXACT || hc->bits != 4 || hc->group != 128 || hc->K % 128 != 0 ||
-        np % 256 != 0)
-        return false;
+    if (!horner_shape(hc)) return false;
     // rounds of 256 tiles: a 256 x 256 round takes about two 128 x 256 rounds, so the Horner grid
     // must not need more rounds than half the fold form's (M = 4300: 2 vs 3 rounds -> fold form)
     const int t256 = ((M + 255) / 256) * (np / 256), t128 = ((M + 127) / 128) * (np / 256);
@@ -1921,39 +1911,6 @@ bool horner_ready(const dllm_linear *hc, int M, hipStream_t st) {
 #endif
     if (t256 < kCUs || 2 * ((t256 + kCUs - 1) / kCUs) > (t128 + kCUs - 1) / kCUs) return false;
     return ensure_horner(hc, st);
-}
-
-// Builds the handle's Horner ratios and decides their validity, once (see horner_ready).
-bool ensure_horner(const dllm_linear *hc, hipStream_t st) {
-    if (hc->precision != DLLM_PRECISION_EXACT || hc->bits != 4 || hc->group != 128 || hc->K % 128 != 0 ||
-        hc->Npad % 256 != 0)
-        return false;
-    dllm_linear *h = const_cast<dllm_linear *>(hc);
-    std::lock_guard<std::mutex> lk(h->mu);
-    if (h->hstate) return h->hstate == 1;
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    (void)hipStreamIsCapturing(st, &cs);
-    if (cs != hipStreamCaptureStatusNone) return false;
-    float *hr = nullptr;
-    int *flag = nullptr, unsafe = 1;
-    if (hipMalloc(reinterpret_cast<void **>(&hr), (h->G + 1) * h->Npad * 4) != hipSuccess) return false;
-    if (hipMalloc(reinterpret_cast<void **>(&flag), sizeof(int)) != hipSuccess) { (void)hipFree(hr); return false; }
-    bool ok = hipMemsetAsync(flag, 0, sizeof(int), st) == hipSuccess;
-    if (ok) {
-        build_horner_kernel<<<static_cast<unsigned>((h->Npad + 255) / 256), 256, 0, st>>>(h->sf, h->G, h->N, h->Npad, hr, flag);
-        ok = hipGetLastError() == hipSuccess &&
-             hipMemcpyAsync(&unsafe, flag, sizeof(int), hipMemcpyDeviceToHost, st) == hipSuccess &&
-             hipStreamSynchronize(st) == hipSuccess;
-    }
-    (void)hipFree(flag);
-    if (!ok || unsafe) {
-        (void)hipFree(hr);
-        if (ok) h->hstate = 2;   // a failed build is retried by the next call
-        return false;
-    }
-    h->hr = hr;
-    h->hstate = 1;
-    return true;
 }
 
 template <typename YT, int EPI>
@@ -2061,6 +2018,7 @@ int alloc_linear(size_t K, size_t N, uint8_t bits, size_t group, int precision, 
     auto A = [&](void **p, size_t bytes) { return hipMalloc(p, std::max<size_t>(bytes, 16)); };
     hipError_t e = hipSuccess;
     if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->wdev), h->Npad * K * bits / 8);
+    if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->wdec), h->Npad * ((K + 127) / 128) * 128 * bits / 8);
     if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->sz), h->G * h->Npad * 4);
     if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->sf), h->G * h->Npad * 4);
     if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->bias), h->Npad * 4);
@@ -2076,7 +2034,10 @@ int alloc_linear(size_t K, size_t N, uint8_t bits, size_t group, int precision, 
 }
 
 // Device layouts from the canonical codes (`canon`, u32-addressable, ceil(K N bits / 32) words)
-// and the scales / zero points [G][N] (all three only read by these launches).
+// and the scales / zero points [G][N] (all three only read by these launches): the prefill and
+// decode code layouts, the {zp, scale} pairs, the f32 scales and, for the Horner-form shapes, the
+// ratios with their validity flag.  Ends with one synchronisation of `st` (create is synchronous:
+// the flag decides the handle's kernel once, and the caller's temporaries may be freed after it).
 int finish_linear(dllm_linear *h, const uint32_t *canon, const float *scales, const uint8_t *zps, const float *bias,
                   hipStream_t st) {
     DLLM_HIP_TRY(hipMemsetAsync(h->bias, 0, h->Npad * 4, st));
@@ -2088,13 +2049,56 @@ int finish_linear(dllm_linear *h, const uint32_t *canon, const float *scales, co
     build_fragments16_kernel<<<gf, 256, 0, st>>>(canon, h->K, h->N, h->Npad, h->bits, h->w16);
     DLLM_LAUNCH_CHECK();
 #endif
+    dim3 gd(static_cast<unsigned>((h->Npad + 255) / 256), static_cast<unsigned>((h->K + 127) / 128));
+    build_decode_from_wdev_kernel<<<gd, 256, 0, st>>>(h->wdev, h->K, h->Npad, h->bits, h->wdec);
+    DLLM_LAUNCH_CHECK();
     dim3 gs(static_cast<unsigned>((h->Npad + 255) / 256), static_cast<unsigned>(h->G));
     build_sz_kernel<<<gs, 256, 0, st>>>(scales, zps, h->G, h->N, h->Npad, h->sz);
     DLLM_LAUNCH_CHECK();
     build_sf_kernel<<<gs, 256, 0, st>>>(scales, h->G, h->N, h->Npad, h->sf);
     DLLM_LAUNCH_CHECK();
+    int *flag = nullptr, unsafe = 1;
+    if (horner_shape(h)) {
+        DLLM_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&h->hr), (h->G + 1) * h->Npad * 4));
+        DLLM_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&flag), sizeof(int)));
+        hipError_t e = hipMemsetAsync(flag, 0, sizeof(int), st);
+        if (e == hipSuccess) {
+            build_horner_kernel<<<static_cast<unsigned>((h->Npad + 255) / 256), 256, 0, st>>>(h->sf, h->G, h->N,
+                                                                                               h->Npad, h->hr, flag);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipMemcpyAsync(&unsafe, flag, sizeof(int), hipMemcpyDeviceToHost, st);
+        if (e != hipSuccess) {
+            (void)hipStreamSynchronize(st);
+            (void)hipFree(flag);
+            return fail(DLLM_ERR_HIP, std::string("Horner ratios: ") + hipGetErrorString(e));
+        }
+    }
+    const hipError_t e = hipStreamSynchronize(st);
+    (void)hipFree(flag);
+    if (e != hipSuccess) return fail(DLLM_ERR_HIP, std::string("linear create: ") + hipGetErrorString(e));
+    if (h->hr) {
+        h->hstate = unsafe ? 2 : 1;
+        if (unsafe) {   // the fold form runs; the ratios are not kept
+            (void)hipFree(h->hr);
+            h->hr = nullptr;
+        }
+    }
     return DLLM_OK;
 }
+
+// Device temporaries of one create (the canonical codes, scales and zero points): owned by that
+// create alone, released after finish_linear's synchronisation.
+struct CreateTemps {
+    void *p[2] = {nullptr, nullptr};
+    ~CreateTemps() {
+        for (void *q : p) (void)hipFree(q);
+    }
+    template <typename T>
+    T *alloc(int i, size_t bytes) {
+        return hipMalloc(&p[i], std::max<size_t>(bytes, 16)) == hipSuccess ? static_cast<T *>(p[i]) : nullptr;
+    }
+};
 
 }  // namespace
 }  // namespace dllm
@@ -2111,12 +2115,12 @@ int dllm_linear_create_ex(const float *W, const float *bias, size_t K, size_t N,
     dllm_linear *h = nullptr;
     if ((rc = alloc_linear(K, N, bits, group, precision, &h))) return rc;
     hipStream_t st = as_stream(stream);
-    // The canonical codes only live for the creation: a per-stream workspace slot (reused by every
-    // create on this stream, in stream order), not handle memory.
+    // The canonical codes, scales and zero points only live for the creation (its own buffers).
     const size_t cbytes = canon_words(K, N, bits) * 4;
-    uint32_t *canon = reinterpret_cast<uint32_t *>(device_workspace(st, cbytes, 3));
-    float *scales = device_workspace(st, h->G * N * 4 + h->G * N, 4);   // scales [G][N] f32, then zps u8
-    if (!canon || !scales) { free_linear(h); return DLLM_ERR_HIP; }
+    CreateTemps tmp;
+    uint32_t *canon = tmp.alloc<uint32_t>(0, cbytes);
+    float *scales = tmp.alloc<float>(1, h->G * N * 4 + h->G * N);   // scales [G][N] f32, then zps u8
+    if (!canon || !scales) { free_linear(h); return fail(DLLM_ERR_HIP, "hipMalloc (create temporaries)"); }
     uint8_t *zps = reinterpret_cast<uint8_t *>(scales + h->G * N);
     hipError_t e = hipMemsetAsync(canon, 0, cbytes, st);
     if (e != hipSuccess) { free_linear(h); return fail(DLLM_ERR_HIP, hipGetErrorString(e)); }
@@ -2150,8 +2154,9 @@ int dllm_linear_create_quantized_ex(const uint8_t *packed_codes, const float *sc
     hipStream_t st = as_stream(stream);
     // The caller's bitstream is read through u32 words: stage it in a zero-padded workspace.
     const size_t nbytes = (K * N * bits + 7) / 8, cbytes = canon_words(K, N, bits) * 4;
-    uint32_t *canon = reinterpret_cast<uint32_t *>(device_workspace(st, cbytes, 3));
-    if (!canon) { free_linear(h); return DLLM_ERR_HIP; }
+    CreateTemps tmp;
+    uint32_t *canon = tmp.alloc<uint32_t>(0, cbytes);
+    if (!canon) { free_linear(h); return fail(DLLM_ERR_HIP, "hipMalloc (create temporaries)"); }
     hipError_t e = hipMemsetAsync(canon, 0, cbytes, st);
     if (e == hipSuccess) e = hipMemcpyAsync(canon, packed_codes, nbytes, hipMemcpyDeviceToDevice, st);
     if (e != hipSuccess) { free_linear(h); return fail(DLLM_ERR_HIP, hipGetErrorString(e)); }
@@ -2308,8 +2313,8 @@ size_t dllm_linear_weight_bytes(dllm_linear_t h) {
 size_t dllm_linear_device_bytes(dllm_linear_t h) {
     if (!h) return 0;
     size_t b = h->Npad * h->K * h->bits / 8 + h->G * h->Npad * 8 + h->Npad * 4;   // wdev, sz + sf, bias
-    if (h->wdec) b += h->Npad * ((h->K + 127) / 128) * 128 * h->bits / 8;          // decode layout, once built
-    if (h->hr) b += (h->G + 1) * h->Npad * 4;                                         // Horner ratios, once built
+    b += h->Npad * ((h->K + 127) / 128) * 128 * h->bits / 8;                       // decode layout
+    if (h->hr) b += (h->G + 1) * h->Npad * 4;                                         // Horner ratios (valid ones)
 #if DLLM_LAB
     b += h->Npad * h->K * h->bits / 8;
 #endif

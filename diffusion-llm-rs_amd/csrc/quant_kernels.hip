@@ -691,10 +691,18 @@ inline int launch_minmax(const float *x, size_t n, float2 *partials, unsigned nb
 
 inline unsigned minmax_blocks(size_t n) { return grid_for((n + 15) / 16, kBlock, kMinmaxBlocks); }
 
-// DLLM_QUANT_GENERIC=1 selects the generic two-kernel path (A/B measurement and parity tests).
+// Lab build only: DLLM_QUANT_GENERIC=1 selects the generic two-kernel path (A/B measurement).  The
+// product library reads no environment; its generic path runs for x not 16-byte aligned.
+#ifndef DLLM_LAB
+#define DLLM_LAB 0
+#endif
 inline bool fused_disabled() {
+#if DLLM_LAB
     const char *e = std::getenv("DLLM_QUANT_GENERIC");
     return e && e[0] == '1';
+#else
+    return false;
+#endif
 }
 
 inline bool fused_width(int b) { return b == 1 || b == 2 || b == 4 || b == 8; }
@@ -1073,6 +1081,23 @@ int dllm_quantize_params_from_extremes(const float *stats, uint8_t bits, float *
     if (bits < 1 || bits > 8) return fail(DLLM_ERR_INVALID_PARAMS, "Bits must be between 1 and 8");
     if (!stats || !params) return fail(DLLM_ERR_INVALID_PARAMS, "null pointer");
     params_from_extremes_kernel<<<1, 64, 0, as_stream(stream)>>>(stats, bits, params);
+    DLLM_LAUNCH_CHECK();
+    return DLLM_OK;
+}
+
+int dllm_quantize_tensor_pair_with_params(const float *x, size_t n, uint8_t bits_a, uint8_t bits_b, int packed,
+                                          const float *params_a, const float *params_b, uint8_t *out_a, uint8_t *out_b,
+                                          dllm_stream_t stream) {
+    // quantization.rs:59-65 at two widths with given device params, one read of x (the head-sharded
+    // KVCacheEntry::update: both copies from one all-reduced pair of extremes).
+    if (bits_a < 1 || bits_a > 8 || bits_b < 1 || bits_b > 8)
+        return fail(DLLM_ERR_INVALID_PARAMS, "Bits must be between 1 and 8");
+    if (!params_a || !params_b || (n && (!x || !out_a || !out_b))) return fail(DLLM_ERR_INVALID_PARAMS, "null pointer");
+    if (!aligned(x, 4)) return fail(DLLM_ERR_INVALID_PARAMS, "x must be 4-byte aligned");
+    if (!n) return DLLM_OK;
+    quantize_pair_kernel<<<octet_grid(n), kBlock, 0, as_stream(stream)>>>(x, n, bits_a, bits_b, packed, out_a, out_b,
+                                                                          params_a, params_b, aligned(x, 16),
+                                                                          aligned(out_a, 8), aligned(out_b, 8));
     DLLM_LAUNCH_CHECK();
     return DLLM_OK;
 }

@@ -246,6 +246,78 @@ struct JReader {
         return ok = false;
     }
     float f32_or_null() { return null() ? NAN : static_cast<float>(number()); }
+    // a JSON string value as UTF-8 (serde_json's string reader: the escapes of RFC 8259 including
+    // \uXXXX surrogate pairs; raw control characters and lone surrogates are errors)
+    bool hex4(unsigned &v) {
+        if (e - p < 4) return false;
+        v = 0;
+        for (int i = 0; i < 4; ++i) {
+            const char c = *p++;
+            v <<= 4;
+            if (c >= '0' && c <= '9') v |= c - '0';
+            else if (c >= 'a' && c <= 'f') v |= c - 'a' + 10;
+            else if (c >= 'A' && c <= 'F') v |= c - 'A' + 10;
+            else return false;
+        }
+        return true;
+    }
+    static void utf8(std::string &o, unsigned cp) {
+        if (cp < 0x80) {
+            o.push_back(static_cast<char>(cp));
+        } else if (cp < 0x800) {
+            o.push_back(static_cast<char>(0xC0 | (cp >> 6)));
+            o.push_back(static_cast<char>(0x80 | (cp & 63)));
+        } else if (cp < 0x10000) {
+            o.push_back(static_cast<char>(0xE0 | (cp >> 12)));
+            o.push_back(static_cast<char>(0x80 | ((cp >> 6) & 63)));
+            o.push_back(static_cast<char>(0x80 | (cp & 63)));
+        } else {
+            o.push_back(static_cast<char>(0xF0 | (cp >> 18)));
+            o.push_back(static_cast<char>(0x80 | ((cp >> 12) & 63)));
+            o.push_back(static_cast<char>(0x80 | ((cp >> 6) & 63)));
+            o.push_back(static_cast<char>(0x80 | (cp & 63)));
+        }
+    }
+    bool string(std::string &o) {
+        ws();
+        if (p >= e || *p != '"') return ok = false;
+        ++p;
+        while (p < e && *p != '"') {
+            const unsigned char c = static_cast<unsigned char>(*p);
+            if (c < 0x20) return ok = false;
+            if (c != '\\') { o.push_back(*p++); continue; }
+            if (++p >= e) return ok = false;
+            const char x = *p++;
+            switch (x) {
+            case '"': o.push_back('"'); break;
+            case '\\': o.push_back('\\'); break;
+            case '/': o.push_back('/'); break;
+            case 'b': o.push_back('\b'); break;
+            case 'f': o.push_back('\f'); break;
+            case 'n': o.push_back('\n'); break;
+            case 'r': o.push_back('\r'); break;
+            case 't': o.push_back('\t'); break;
+            case 'u': {
+                unsigned cp;
+                if (!hex4(cp)) return ok = false;
+                if (cp >= 0xDC00 && cp <= 0xDFFF) return ok = false;
+                if (cp >= 0xD800 && cp <= 0xDBFF) {
+                    unsigned lo;
+                    if (e - p < 6 || p[0] != '\\' || p[1] != 'u') return ok = false;
+                    p += 2;
+                    if (!hex4(lo) || lo < 0xDC00 || lo > 0xDFFF) return ok = false;
+                    cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+                }
+                utf8(o, cp);
+                break;
+            }
+            default: return ok = false;
+            }
+        }
+        if (p >= e) return ok = false;
+        ++p;
+        return true;
+    }
 };
 
 int parse_params(JReader &j, dllm_qparams *p) {
@@ -447,6 +519,44 @@ int dllm_compressed_vector_to_json(const char *id, size_t id_len, const uint8_t 
                           std::to_string(static_cast<unsigned>(bits)) + ",\"original_shape\":" + json_usizes(shape, ndim) +
                           ",\"quant_scale\":" + json_f32(scale) + ",\"quant_zero_point\":" + json_f32(zero_point) + "}";
     return emit(s, out, cap, len);
+}
+
+int dllm_compressed_vector_from_json(const char *s, size_t len, char *id, size_t id_cap, size_t *id_len,
+                                     uint8_t *data, size_t data_cap, size_t *n, uint8_t *bits, uint64_t *shape,
+                                     size_t shape_cap, size_t *ndim, float *scale, float *zero_point) {
+    if ((!s && len) || !id_len || !n || !bits || !ndim || !scale || !zero_point)
+        return fail(DLLM_ERR_INVALID_PARAMS, "null argument");
+    JReader j{s, s + len};
+    std::string ident;
+    std::vector<uint8_t> codes;
+    std::vector<uint64_t> dims;
+    bool seen[6] = {false, false, false, false, false, false};
+    j.expect('{');
+    do {
+        const std::string k = j.key();
+        long long v;
+        if (k == "id") { j.string(ident); seen[0] = true; }
+        else if (k == "data") { j.int_array<uint8_t>(0, 255, codes); seen[1] = true; }
+        else if (k == "bits") { if (j.integer(0, 255, v)) *bits = static_cast<uint8_t>(v); seen[2] = true; }
+        else if (k == "original_shape") { j.int_array<uint64_t>(0, INT64_MAX, dims); seen[3] = true; }
+        else if (k == "quant_scale") { *scale = j.f32_or_null(); seen[4] = true; }
+        else if (k == "quant_zero_point") { *zero_point = j.f32_or_null(); seen[5] = true; }
+        else j.ok = false;
+    } while (j.ok && j.lit(","));
+    j.expect('}');
+    j.ws();
+    if (!j.ok || j.p != j.e) return fail(DLLM_ERR_SERIALIZATION, "json: malformed CompressedVector");
+    for (bool v : seen)
+        if (!v) return fail(DLLM_ERR_SERIALIZATION, "json: missing field of CompressedVector");
+    *id_len = ident.size();
+    *n = codes.size();
+    *ndim = dims.size();
+    if ((id && id_cap < ident.size()) || (data && data_cap < codes.size()) || (shape && shape_cap < dims.size()))
+        return fail(DLLM_ERR_INVALID_PARAMS, "output buffer too small (see the counts)");
+    if (id && !ident.empty()) std::memcpy(id, ident.data(), ident.size());
+    if (data && !codes.empty()) std::memcpy(data, codes.data(), codes.size());
+    if (shape && !dims.empty()) std::memcpy(shape, dims.data(), dims.size() * 8);
+    return DLLM_OK;
 }
 
 }  // extern "C"

@@ -173,10 +173,18 @@ class KVCacheEntry:
     def __init__(self, keys: torch.Tensor, values: torch.Tensor, prefill_bits: int, decode_bits: int):
         self.keys, self.values = keys, values
         self.prefill_quant_bits, self.decode_quant_bits = prefill_bits, decode_bits
-        self.prefill_quantized = QuantizedKVCacheEntry.new(keys, values, prefill_bits) if prefill_bits > 0 else None
-        self.decode_quantized = QuantizedKVCacheEntry.new(keys, values, decode_bits) if decode_bits > 0 else None
+        self.prefill_quantized = self._quantize(keys, values, prefill_bits) if prefill_bits > 0 else None
+        self.decode_quantized = self._quantize(keys, values, decode_bits) if decode_bits > 0 else None
         self.is_prefill_phase = True
         self.seq_len = int(keys.shape[1])
+
+    # The quantization steps (QuantizedKVCacheEntry::new at one width, or at two widths in one pass);
+    # parallel.HeadParallelKVCacheEntry overrides them with the head-sharded form.
+    def _quantize(self, keys, values, bits):
+        return QuantizedKVCacheEntry.new(keys, values, bits)
+
+    def _quantize_pair(self, keys, values, bits_a, bits_b):
+        return QuantizedKVCacheEntry.new_pair(keys, values, bits_a, bits_b)
 
     @classmethod
     def new(cls, keys, values, prefill_bits, decode_bits):
@@ -187,11 +195,15 @@ class KVCacheEntry:
 
     def get_keys(self) -> torch.Tensor:
         q = self._current()
-        return self.keys.clone() if q is None else q.dequantize_keys()
+        return self.keys.clone() if q is None else self._dequantize(q.keys)
 
     def get_values(self) -> torch.Tensor:
         q = self._current()
-        return self.values.clone() if q is None else q.dequantize_values()
+        return self.values.clone() if q is None else self._dequantize(q.values)
+
+    def _dequantize(self, t):
+        """QuantizedKVCacheEntry::dequantize_keys/values (quantization.rs:160-175)."""
+        return t.dequantize().reshape(t.shape)
 
     def get_current_quant_bits(self) -> int:
         return self.prefill_quant_bits if self.is_prefill_phase else self.decode_quant_bits
@@ -205,7 +217,7 @@ class KVCacheEntry:
             return
         self.is_prefill_phase = is_prefill
         if not is_prefill and self.decode_quant_bits > 0 and self.decode_quantized is None:
-            self.decode_quantized = QuantizedKVCacheEntry.new(self.keys, self.values, self.decode_quant_bits)
+            self.decode_quantized = self._quantize(self.keys, self.values, self.decode_quant_bits)
 
     def update(self, new_keys: torch.Tensor, new_values: torch.Tensor):
         """lib.rs:241-276 (the missing QuantizedKVCacheEntry::update is a re-quantization)."""
@@ -213,17 +225,17 @@ class KVCacheEntry:
         self.seq_len = int(new_keys.shape[1])
         if self.prefill_quant_bits > 0 and self.decode_quant_bits > 0:
             # both widths from one min/max pass and one read per tensor (bit-identical)
-            self.prefill_quantized, self.decode_quantized = QuantizedKVCacheEntry.new_pair(
+            self.prefill_quantized, self.decode_quantized = self._quantize_pair(
                 new_keys, new_values, self.prefill_quant_bits, self.decode_quant_bits)
             return
         if self.prefill_quant_bits > 0:
-            self.prefill_quantized = QuantizedKVCacheEntry.new(new_keys, new_values, self.prefill_quant_bits)
+            self.prefill_quantized = self._quantize(new_keys, new_values, self.prefill_quant_bits)
         if self.decode_quant_bits > 0:
-            self.decode_quantized = QuantizedKVCacheEntry.new(new_keys, new_values, self.decode_quant_bits)
+            self.decode_quantized = self._quantize(new_keys, new_values, self.decode_quant_bits)
 
     def clone(self) -> "KVCacheEntry":
         """``#[derive(Clone)]``: an independent copy (device tensors duplicated)."""
-        c = object.__new__(KVCacheEntry)
+        c = object.__new__(type(self))
         c.__dict__.update(self.__dict__)
         c.keys, c.values = self.keys.clone(), self.values.clone()
         c.prefill_quantized = None if self.prefill_quantized is None else self.prefill_quantized.clone()
@@ -360,6 +372,20 @@ def progressive_bits(config: DiffusionConfig, num_steps: int, t: int) -> int:
     return int(min(max(np.trunc(v), 0), 255))
 
 
+class DeviceLoopOps:
+    """The loop's elementwise steps as HIP kernels behind the C-ABI (the product path)."""
+
+    @staticmethod
+    def p_sample(x, eps, noise, coef, flag, seed, offset, out):
+        """lib.rs:1152-1215 over x as one sample of x.numel() elements (coef = device f32 [1, 3])."""
+        check(_lib.load().dllm_p_sample(_ptr(x), _ptr(eps), None if noise is None else _ptr(noise), _ptr(coef), 1,
+                                        x.numel(), int(flag), seed, offset, _ptr(out), _stream()))
+
+    @staticmethod
+    def randn(out, seed, offset):
+        check(_lib.load().dllm_randn(seed, offset, _ptr(out), out.numel(), _stream()))
+
+
 class DenoiseLoop:
     """DiffuseLLM::sample (lib.rs:853-955) over an L-layer quantized denoiser (config C5).
 
@@ -378,13 +404,24 @@ class DenoiseLoop:
     layer has forward_psample), or on the side stream into one of two buffers (noise="side"; the
     last layer then waits for it).  Every form is bit-identical to overlap=False.  Measured at
     config C5 (scripts/c5_ab.py): epilogue 0.922, side 0.953, serial 0.963 ms per step -- the
-    side-stream draw costs the GEMMs more CU time than the in-epilogue draw costs the last layer."""
+    side-stream draw costs the GEMMs more CU time than the in-epilogue draw costs the last layer.
+
+    The layers may be tensor-parallel (parallel.TensorParallelPair: one reduction per pair, x
+    replicated on every rank) and the cache head-sharded (parallel.HeadParallelKVCacheEntry): every
+    rank then runs this same loop on its shards, with the same phase, width and noise sequence.
+    ``ops`` holds the elementwise steps (p_sample, noise) and ``device`` where x lives: the HIP
+    kernels on the GPU (``DeviceLoopOps``); the CPU multi-process tests pass the oracle's
+    restatement and device "cpu" (serial schedule only)."""
 
     def __init__(self, layers: Sequence, config: DiffusionConfig, cumprod: Cumprod = Cumprod.INCLUSIVE,
                  alpha_mode: AlphaMode = AlphaMode.PER_SAMPLE, seed: int = 0,
-                 kv_cache: Optional[KVCacheEntry] = None, overlap: bool = True, noise: str = "epilogue"):
+                 kv_cache: Optional[KVCacheEntry] = None, overlap: bool = True, noise: str = "epilogue",
+                 ops=DeviceLoopOps, device="cuda"):
         if noise not in ("side", "epilogue"):
             raise ValueError("noise must be 'side' or 'epilogue'")
+        self.ops, self.device = ops, torch.device(device)
+        if self.device.type != "cuda":
+            overlap = False
         self.layers = list(layers)
         self.noise_mode = noise if self.layers and hasattr(self.layers[-1], "forward_psample") else "side"
         self.config = config
@@ -403,7 +440,7 @@ class DenoiseLoop:
             tt = np.asarray([t], np.uint64)
             check(_lib.load().dllm_p_sample_coeffs(_ptr(self._betas), self._betas.size, int(self.cumprod),
                                                    int(self.alpha_mode), _ptr(tt), 1, _ptr(coef), C.byref(flag)))
-            self._coef_cache[t] = (torch.from_numpy(coef).cuda(), bool(flag.value))
+            self._coef_cache[t] = (torch.from_numpy(coef).to(self.device), bool(flag.value))
         return self._coef_cache[t]
 
     def step(self, x: torch.Tensor, t: int, step_index: int, out: Optional[torch.Tensor] = None,
@@ -422,8 +459,7 @@ class DenoiseLoop:
             last.forward_psample(h, x, coef, M, flag, self.seed, offset, out, noise=noise)
         else:
             eps = last(h, out_dtype=torch.float32)
-            check(_lib.load().dllm_p_sample(_ptr(x), _ptr(eps), None if noise is None else _ptr(noise), _ptr(coef),
-                                            1, M * d, int(flag), self.seed, offset, _ptr(out), _stream()))
+            self.ops.p_sample(x, eps, noise, coef, flag, self.seed, offset, out)
         return out
 
     def kv_step(self, t: int, num_steps: int):
@@ -462,7 +498,7 @@ class DenoiseLoop:
 
     def _sample(self, x: torch.Tensor, num_steps: Optional[int] = None) -> torch.Tensor:
         num_steps = num_steps or self.config.num_timesteps
-        x = x.to(device="cuda", dtype=torch.float32).contiguous()
+        x = x.to(device=self.device, dtype=torch.float32).contiguous()
         buf = torch.empty_like(x)
         M, d = x.shape
         main = torch.cuda.current_stream()
@@ -491,7 +527,7 @@ class DenoiseLoop:
             with torch.cuda.stream(side):
                 if freed[j] is not None:
                     side.wait_event(freed[j])
-                check(_lib.load().dllm_randn(self.seed, i * M * d, _ptr(nz), M * d, _stream()))
+                self.ops.randn(nz, self.seed, i * M * d)
                 ready = torch.cuda.Event()
                 ready.record(side)
                 self.kv_step(t, num_steps)

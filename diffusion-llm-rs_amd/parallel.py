@@ -21,8 +21,12 @@ straddle a column boundary and K/G is a whole number of groups for G <= 32.  Mod
 
 ``shard=(world, rank)`` builds the shard rank ``rank`` of a ``world``-way split in a process that
 is not part of such a group and disables the collectives (``partial`` gives the un-reduced
-output): the one-process emulation the GPU parity tests use to compose the HIP GEMM with the
-partition logic.  The local GEMM is pluggable (``local_factory``): on the GPU it is ``QuantLinear``
+output; a row shard's ``forward`` refuses, since its output would lack the other ranks' sums and
+carry the whole bias): the one-process emulation the GPU parity tests use to compose the HIP GEMM
+with the partition logic.  ``EmulatedTensorParallel`` and ``EmulatedHeadParallelKV`` put all G
+shards of a layer / of the KV cache behind the unsharded interface, replacing each collective by
+its definition (f32 sum of the partials in rank order; max of the extremes), so that a whole
+``DenoiseLoop`` runs sharded in one process.  The local GEMM is pluggable (``local_factory``): on the GPU it is ``QuantLinear``
 (HIP kernels); the CPU multi-process tests pass the oracle's restatement so the partition and
 collective logic is checked under gloo without a GPU.
 """
@@ -32,6 +36,9 @@ from typing import Callable, Optional
 
 import torch
 import torch.distributed as dist
+
+from .diffusion import KVCacheEntry
+from .quantization import QuantizedKVCacheEntry, QuantizedTensor
 
 
 def _world(pg=None, shard=None):
@@ -131,6 +138,9 @@ class RowParallelLinear:
         Rows are independent, so every chunking gives the same per-row partial sums."""
         xs = x if x_is_shard else x[:, self.k0:self.k1].contiguous()
         if not self.collective:
+            if self.world > 1:   # shard emulation: the reduction belongs to the caller
+                raise ValueError("a row shard's forward needs the reduction over its ranks: use partial() "
+                                 "(or EmulatedTensorParallel) under shard=(world, rank)")
             return self._finish(self.partial(xs, True), out_dtype)
         if self.reduce == "rs_ag":
             return self._forward_rs_ag(xs, out_dtype, chunks)
@@ -259,6 +269,15 @@ class DeviceKVOps:
         return quantize_tensor_with_params(x, bits, params, packed=True)
 
     @staticmethod
+    def dequantize(t):
+        return t.dequantize().reshape(t.shape)
+
+    @staticmethod
+    def quantize_pair(x, bits_a, bits_b, params_a, params_b):
+        from .quantization import quantize_tensor_pair_with_params
+        return quantize_tensor_pair_with_params(x, bits_a, bits_b, params_a, params_b, packed=True)
+
+    @staticmethod
     def attention(q, k, v):
         from .quantization import kv_attention
         return kv_attention(q, k, v)
@@ -315,3 +334,218 @@ class HeadParallelKVCache:
     def attention(self, q_local: torch.Tensor, entry) -> torch.Tensor:
         """Dequant-attention of the local heads: O[:, h0:h1, :] of the unsharded call."""
         return self.ops.attention(q_local, entry.keys, entry.values)
+
+
+# ---- config C5 sharded as a whole loop: the phase-aware KV cache by head, emulation helpers ----------
+
+def head_columns(hidden: int, num_heads: int, world: int, rank: int):
+    """Hidden-column shard [c0, c1) of rank ``rank``: its heads [h0, h1) (head_range) times head_dim
+    (hidden = num_heads * head_dim, the K/V layout [layers, seq, heads * head_dim] of
+    init_kv_cache, diffuse-llm-rs/src/lib.rs:958-980)."""
+    if hidden % num_heads:
+        raise ValueError("hidden size must be a whole number of heads")
+    hd = hidden // num_heads
+    h0, h1 = head_range(num_heads, world, rank)
+    return h0 * hd, h1 * hd
+
+
+class HeadParallelKVCacheEntry(KVCacheEntry):
+    """``KVCacheEntry`` (diffuse-llm-rs/src/lib.rs:121-313: f32 K/V plus a prefill-width and a
+    decode-width per-tensor quantized copy, phase switch, progressive decode widths, re-quantizing
+    ``update``) with K and V sharded by head over the ranks: rank r holds the hidden
+    columns of its heads (``head_columns``) of K, V ``[layers, seq, hidden]`` as contiguous local
+    tensors.  The phase logic and the accounting (lib.rs:279-302, per shard) are KVCacheEntry's.
+
+    The reference quantizes K and V per WHOLE tensor (quantization.rs:142-150), so a shard's
+    params need the global extremes: each quantization folds the local K and V (NaN-ignoring,
+    order-independent, :41-46), combines {-min_K, max_K, -min_V, max_V} over the ranks with ONE
+    ``all_reduce(MAX)`` of 4 floats, and derives the params of every width it writes from that one
+    result (:49-56) -- an update's prefill and decode copies come from the same reduction, both
+    widths written in one read of the shard (dllm_quantize_tensor_pair_with_params).  Codes and
+    params are bit-identical to the unsharded entry's for the shard's elements.
+    ``transition_phase`` re-quantizes the same K/V the last quantization reduced, so it reuses that
+    reduction (no collective; bit-identical).  ``red``: extremes already reduced over the ranks
+    (the one-process emulation supplies them); ``ops``: the per-shard device steps
+    (``DeviceKVOps``; the CPU gloo tests pass the oracle's)."""
+
+    def __init__(self, keys_local, values_local, prefill_bits, decode_bits, pg=None, ops=DeviceKVOps,
+                 red=None):
+        self.pg, self.ops = pg, ops
+        self.world, self.rank = _world(pg)
+        self._red_next = red       # the emulation's pre-reduced extremes for the next quantization
+        self._red_of = None        # (keys, values, reduced extremes) of the last quantization
+        self._reuse = True         # the constructor's two widths share one reduction
+        super().__init__(keys_local, values_local, prefill_bits, decode_bits)
+        self._reuse = False
+
+    def transition_phase(self, is_prefill: bool):
+        """lib.rs:221-239; a decode copy made here quantizes the K/V of the last reduction."""
+        self._reuse = True
+        try:
+            super().transition_phase(is_prefill)
+        finally:
+            self._reuse = False
+
+    def update(self, new_keys, new_values):
+        """lib.rs:241-276: one fresh reduction of the new K/V for both widths."""
+        self._red_of = None
+        super().update(new_keys, new_values)
+
+    def local_extremes(self, keys, values):
+        """This shard's {-min_K, max_K, -min_V, max_V} (the all-reduce operand; NaN skipped)."""
+        return _local_extremes_of(keys, values, self.ops)
+
+    def _reduced(self, keys, values):
+        last = self._red_of
+        if self._reuse and last is not None and last[0] is keys and last[1] is values:
+            return last[2]
+        if self._red_next is not None:
+            red, self._red_next = self._red_next, None
+        else:
+            red = self.local_extremes(keys, values)
+            if self.world > 1:
+                dist.all_reduce(red, op=dist.ReduceOp.MAX, group=self.pg)
+        self._red_of = (keys, values, red)
+        return red
+
+    def _dequantize(self, t):
+        return self.ops.dequantize(t)
+
+    def _params(self, red, bits):
+        return (self.ops.params(torch.stack([-red[0], red[1]]), bits),
+                self.ops.params(torch.stack([-red[2], red[3]]), bits))
+
+    def _entry(self, keys, values, kc, kp, vc, vp, bits):
+        seq = int(keys.shape[1]) if keys.dim() > 1 else 0
+        return QuantizedKVCacheEntry(QuantizedTensor(kc, tuple(keys.shape), kp, int(bits), True),
+                                     QuantizedTensor(vc, tuple(values.shape), vp, int(bits), True), seq)
+
+    def _quantize(self, keys, values, bits):
+        kp, vp = self._params(self._reduced(keys, values), bits)
+        return self._entry(keys, values, self.ops.quantize(keys, bits, kp), kp, self.ops.quantize(values, bits, vp),
+                           vp, bits)
+
+    def _quantize_pair(self, keys, values, bits_a, bits_b):
+        red = self._reduced(keys, values)
+        (kpa, vpa), (kpb, vpb) = self._params(red, bits_a), self._params(red, bits_b)
+        kca, kcb = self.ops.quantize_pair(keys, bits_a, bits_b, kpa, kpb)
+        vca, vcb = self.ops.quantize_pair(values, bits_a, bits_b, vpa, vpb)
+        return (self._entry(keys, values, kca, kpa, vca, vpa, bits_a),
+                self._entry(keys, values, kcb, kpb, vcb, vpb, bits_b))
+
+
+class EmulatedHeadParallelKV:
+    """All G head shards of one KV cache entry in one process behind KVCacheEntry's interface (what
+    ``DenoiseLoop.kv_step`` calls): each quantization folds every shard's extremes, takes their max
+    (the all_reduce(MAX) by definition) and hands it to every shard.  ``keys``/``values`` are the
+    lists of shard tensors; ``get_keys``/``get_values`` concatenate the shards' hand-outs along the
+    hidden dimension (the unsharded entry's tensor, for comparison)."""
+
+    def __init__(self, keys, values, prefill_bits, decode_bits, num_heads, world, ops=DeviceKVOps):
+        hidden = keys.shape[-1]
+        self.world, self.num_heads = world, num_heads
+        self.cols = [head_columns(hidden, num_heads, world, r) for r in range(world)]
+        ks = [keys[..., c0:c1].contiguous() for c0, c1 in self.cols]
+        vs = [values[..., c0:c1].contiguous() for c0, c1 in self.cols]
+        red = torch.stack([_local_extremes_of(k, v, ops) for k, v in zip(ks, vs)]).amax(0)
+        self.shards = [HeadParallelKVCacheEntry(k, v, prefill_bits, decode_bits, ops=ops, red=red) for k, v in zip(ks, vs)]
+
+    def _reduce_for(self, keys, values):
+        red = torch.stack([s.local_extremes(k, v) for s, k, v in zip(self.shards, keys, values)]).amax(0)
+        for s in self.shards:
+            s._red_next = red
+
+    # -- KVCacheEntry's interface ------------------------------------------------------------------
+    keys = property(lambda self: [s.keys for s in self.shards])
+    values = property(lambda self: [s.values for s in self.shards])
+    is_prefill_phase = property(lambda self: self.shards[0].is_prefill_phase)
+    prefill_quant_bits = property(lambda self: self.shards[0].prefill_quant_bits)
+
+    @property
+    def decode_quant_bits(self):
+        return self.shards[0].decode_quant_bits
+
+    @decode_quant_bits.setter
+    def decode_quant_bits(self, b):
+        for s in self.shards:
+            s.decode_quant_bits = b
+
+    @property
+    def decode_quantized(self):
+        return [s.decode_quantized for s in self.shards] if self.shards[0].decode_quantized is not None else None
+
+    @decode_quantized.setter
+    def decode_quantized(self, v):
+        if v is not None:
+            raise ValueError("only None (drop the decode copy, lib.rs:900-903) can be assigned")
+        for s in self.shards:
+            s.decode_quantized = None
+
+    @property
+    def prefill_quantized(self):
+        return [s.prefill_quantized for s in self.shards] if self.shards[0].prefill_quantized is not None else None
+
+    def set_phase(self, is_prefill: bool):
+        for s in self.shards:
+            s.set_phase(is_prefill)
+
+    transition_phase = set_phase
+
+    def get_current_quant_bits(self) -> int:
+        return self.shards[0].get_current_quant_bits()
+
+    def get_keys(self):
+        return torch.cat([s.get_keys() for s in self.shards], dim=-1)
+
+    def get_values(self):
+        return torch.cat([s.get_values() for s in self.shards], dim=-1)
+
+    def update(self, new_keys, new_values):
+        """KVCacheEntry::update of every shard; ``new_keys``/``new_values`` are the shard lists (as
+        ``keys``/``values`` hand them out) or full tensors, which are split by head here."""
+        if isinstance(new_keys, torch.Tensor):
+            new_keys = [new_keys[..., c0:c1].contiguous() for c0, c1 in self.cols]
+            new_values = [new_values[..., c0:c1].contiguous() for c0, c1 in self.cols]
+        self._reduce_for(new_keys, new_values)
+        for s, k, v in zip(self.shards, new_keys, new_values):
+            s.update(k, v)
+
+    def memory_usage(self) -> int:
+        return sum(s.memory_usage() for s in self.shards)
+
+    def __len__(self):
+        return len(self.shards[0])
+
+
+def _local_extremes_of(keys, values, ops=DeviceKVOps):
+    sk, sv = ops.extremes(keys), ops.extremes(values)
+    return torch.stack([-sk[0], sk[1], -sv[0], sv[1]]).contiguous()
+
+
+
+class EmulatedTensorParallel:
+    """All G shards of a tensor-parallel layer (``TensorParallelPair`` or ``RowParallelLinear``
+    built with ``shard=(G, r)``) in one process behind the unsharded layer's call: the f32 partials
+    summed in rank order (the all-reduce by definition), then the bias once and the output cast --
+    what every rank holds after the pair's reduction."""
+
+    def __init__(self, shards):
+        self.shards = list(shards)
+        last = self.shards[0]
+        self.bias = (last.b if isinstance(last, TensorParallelPair) else last).bias
+
+    def __call__(self, x, out_dtype=torch.float16):
+        tot = None
+        for s in self.shards:
+            p = s.partial(x)
+            tot = p if tot is None else tot.add_(p)
+        if self.bias is not None:
+            tot = tot + self.bias.to(tot.device, torch.float32)[None, :]
+        return tot.to(out_dtype)
+
+    forward = __call__
+
+    def close(self):
+        for s in self.shards:
+            if hasattr(s, "close"):
+                s.close()

@@ -121,6 +121,25 @@ def quantize_tensor_with_params(data: torch.Tensor, bits: int, params: torch.Ten
     return out
 
 
+def quantize_tensor_pair_with_params(data: torch.Tensor, bits_a: int, bits_b: int, params_a: torch.Tensor,
+                                     params_b: torch.Tensor, packed: bool = False):
+    """:func:`quantize_tensor_with_params` at two widths in one read of ``data`` (the prefill and
+    decode copies of a head-sharded KVCacheEntry::update, diffuse-llm-rs/src/lib.rs:246-276).
+    Returns ``(codes_a, codes_b)``, bit-identical to two single-width calls."""
+    for b in (bits_a, bits_b):
+        if not 1 <= int(b) <= 8:
+            raise _lib.InvalidParams("Bits must be between 1 and 8")
+    x = _dev(data, torch.float32).reshape(-1)
+    n = x.numel()
+    pa, pb = _dev(params_a, torch.float32), _dev(params_b, torch.float32)
+    outs = [torch.empty(packed_bytes(n, b) if packed else n, dtype=torch.uint8, device=x.device) for b in (bits_a, bits_b)]
+    ptr = lambda t: _ptr(t) if t.numel() else None  # noqa: E731
+    check(_lib.load().dllm_quantize_tensor_pair_with_params(_ptr(x) if n else None, n, bits_a, bits_b, int(packed),
+                                                            _ptr(pa), _ptr(pb), ptr(outs[0]), ptr(outs[1]),
+                                                            _stream()))
+    return outs[0], outs[1]
+
+
 def dequantize_tensor(codes: torch.Tensor, scale, zero_point=None, *, bits: int = 8, packed: bool = False,
                       n: int | None = None, out_dtype=torch.float32) -> torch.Tensor:
     """quantization.rs:81-85 ``dequantize_tensor(data, scale, zero_point)``.

@@ -6,21 +6,14 @@ produce for the checkpoint / hand-off structs, in both encodings its crates use.
 * ``PrefillCompressedVector`` -- diffusion_prefill/src/prefill_kv.rs:25-33 (the KV hand-off record
   with its per-vector quant_scale / quant_zero_point), built from ``kvquant.compress_vectors``.
 
-Encodings (third-party, absent from the container; restated from their published specifications):
-* bincode 1.3 ``bincode::serialize`` (legacy config): little-endian, fixed-width integers, usize as
-  u64, Vec / String = u64 length + elements, bool = 1 byte, Option = 1-byte tag (+ value).
-* serde_json ``to_string``: compact, struct fields in declaration order, Vec<u8> as an array of
-  integers, None as null, f32 via ryu's shortest round-trip digits in ryu's layout (non-finite
-  f32 serialises as null).  Deserialising parses the number as f64 and rounds to f32 (serde's
-  f32 visitor), which ``float`` + ``np.float32`` reproduces.
-The byte layout is pinned by these specifications only (the reference ships no serialized
-fixture): parity unpinned beyond the spec-derived tests in tests/test_serde.py.
-Host-side format code: device tensors are copied to / from the host around it.
+Every encoder and decoder here is the library's C-ABI (csrc/serde.cpp, include/dllm_quant.h
+section f3: bincode 1.3 legacy layout, serde_json compact form with ryu's f32 digits); this module
+only moves host buffers across it.  Device tensors are copied to / from the host around it.  The
+independent restatement that checks these bytes is ``oracle/serde_ref.py`` (tests only).
 """
 from __future__ import annotations
 
-import json
-import struct
+import ctypes as C
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -28,196 +21,113 @@ import numpy as np
 import torch
 
 from . import _lib
+from ._lib import check
 from .quant import QuantizationParams, QuantizedTensor
 
-F32 = np.float32
+
+class _QP(C.Structure):
+    """``dllm_qparams``."""
+    _fields_ = [("bits", C.c_uint8), ("scale", C.c_float), ("zero_point", C.c_int32), ("symmetric", C.c_uint8),
+                ("has_axis", C.c_uint8), ("axis", C.c_uint64)]
 
 
-# ---- ryu f32 formatting (serde_json's float writer) ----------------------------------------------
+def _qp(p: QuantizationParams) -> _QP:
+    return _QP(int(p.bits), float(p.scale), int(p.zero_point), int(bool(p.symmetric)), 0 if p.axis is None else 1,
+               0 if p.axis is None else int(p.axis))
+
+
+def _params(q: _QP) -> QuantizationParams:
+    return QuantizationParams(bits=int(q.bits), scale=float(np.float32(q.scale)), zero_point=int(q.zero_point),
+                              symmetric=bool(q.symmetric), axis=int(q.axis) if q.has_axis else None)
+
+
+def _emit(fn, *args) -> bytes:
+    """An encoder call: size query, then the write."""
+    n = C.c_size_t()
+    check(fn(*args, None, 0, C.byref(n)))
+    buf = C.create_string_buffer(max(1, n.value))
+    check(fn(*args, buf, n.value, C.byref(n)))
+    return buf.raw[: n.value]
+
+
+def _u8(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, np.uint8).ravel())
+
+
+def _shape(shape):
+    return (C.c_uint64 * max(1, len(shape)))(*[int(s) for s in shape])
+
 
 def ryu_f32(x) -> str:
-    """Rust ``ryu::Buffer::format_finite(f32)`` (ryu/src/pretty/mod.rs format32)."""
-    x = F32(x)
-    if not np.isfinite(x):
+    """serde_json's text of a finite f32 (ryu's shortest round-trip digits; dllm_format_f32)."""
+    if not np.isfinite(np.float32(x)):
         raise ValueError("non-finite")
-    bits = int(np.asarray(x).view(np.uint32))
-    sign = "-" if bits >> 31 else ""
-    if bits & 0x7FFFFFFF == 0:
-        return sign + "0.0"
-    sci = np.format_float_scientific(abs(x), unique=True, trim="-", exp_digits=1)
-    mant, exp = sci.split("e")
-    digits = mant.replace(".", "")
-    digits = digits.rstrip("0") or "0"
-    length = len(digits)
-    e10 = int(exp)                 # value = d.ddd * 10^e10
-    k = e10 - (length - 1)         # value = digits * 10^k
-    kk = length + k                # 10^(kk-1) <= value < 10^kk
-    if 0 <= k and kk <= 13:
-        out = digits + "0" * (kk - length) + ".0"
-    elif 0 < kk <= 13:
-        out = digits[:kk] + "." + digits[kk:]
-    elif -6 < kk <= 0:
-        out = "0." + "0" * (-kk) + digits
-    elif length == 1:
-        out = digits + "e" + str(kk - 1)
-    else:
-        out = digits[0] + "." + digits[1:] + "e" + str(kk - 1)
-    return sign + out
-
-
-def _json_f32(x):
-    x = F32(x)
-    return "null" if not np.isfinite(x) else ryu_f32(x)
-
-
-def _json_u8_array(a: np.ndarray) -> str:
-    return "[" + ",".join(str(int(v)) for v in a) + "]"
-
-
-# ---- bincode primitives ----------------------------------------------------------------------------
-
-class _Reader:
-    def __init__(self, b: bytes, strict: bool = False):
-        self.b, self.i, self.strict = memoryview(b), 0, strict
-
-    def take(self, n):
-        if self.i + n > len(self.b):
-            raise _lib.SerializationError("bincode: unexpected end of input")
-        v = self.b[self.i:self.i + n]
-        self.i += n
-        return bytes(v)
-
-    def u8(self):
-        return self.take(1)[0]
-
-    def u64(self):
-        return struct.unpack("<Q", self.take(8))[0]
-
-    def i32(self):
-        return struct.unpack("<i", self.take(4))[0]
-
-    def f32(self):
-        return F32(struct.unpack("<f", self.take(4))[0])
-
-    def bool(self):
-        v = self.u8()
-        if v > 1:
-            raise _lib.SerializationError(f"bincode: invalid bool {v}")
-        return bool(v)
-
-    def bytes_vec(self):
-        return np.frombuffer(self.take(self.u64()), dtype=np.uint8).copy()
-
-    def usize_vec(self):
-        n = self.u64()
-        return [self.u64() for _ in range(n)]
-
-    def string(self):
-        return self.take(self.u64()).decode("utf-8")
-
-    def done(self):
-        """bincode 1.3's ``bincode::deserialize`` (the legacy free function the reference's
-        ``bincode`` error conversion serves, quantization/src/error.rs:44-47) is
-        ``DefaultOptions::new().with_fixint_encoding().allow_trailing_bytes()``: bytes after the
-        value are ignored, not an error.  ``strict=True`` readers reject them (the
-        ``DefaultOptions`` default)."""
-        if self.strict and self.i != len(self.b):
-            raise _lib.SerializationError("bincode: trailing bytes")
-
-
-def _b_params(p: QuantizationParams) -> bytes:
-    out = struct.pack("<Bfi?", int(p.bits), float(F32(p.scale)), int(p.zero_point), bool(p.symmetric))
-    out += b"\x00" if p.axis is None else b"\x01" + struct.pack("<Q", int(p.axis))
-    return out
-
-
-def _r_params(r: _Reader) -> QuantizationParams:
-    bits, scale, zp, sym = r.u8(), r.f32(), r.i32(), r.bool()
-    tag = r.u8()
-    if tag > 1:
-        raise _lib.SerializationError(f"bincode: invalid Option tag {tag}")
-    axis = None if tag == 0 else r.u64()
-    return QuantizationParams(bits=bits, scale=float(scale), zero_point=zp, symmetric=sym, axis=axis)
-
-
-def _b_usize_vec(v) -> bytes:
-    return struct.pack("<Q", len(v)) + b"".join(struct.pack("<Q", int(x)) for x in v)
-
-
-def _b_bytes(a: np.ndarray) -> bytes:
-    a = np.ascontiguousarray(a, np.uint8).ravel()
-    return struct.pack("<Q", a.size) + a.tobytes()
+    return _emit(_lib.load().dllm_format_f32, C.c_float(float(x))).decode()
 
 
 # ---- QuantizationParams ------------------------------------------------------------------------------
 
 def params_to_bincode(p: QuantizationParams) -> bytes:
-    return _b_params(p)
+    q = _qp(p)
+    return _emit(_lib.load().dllm_qparams_to_bincode, C.byref(q))
 
 
 def params_from_bincode(b: bytes, strict: bool = False) -> QuantizationParams:
-    r = _Reader(b, strict)
-    p = _r_params(r)
-    r.done()
-    return p
-
-
-def _params_json(p: QuantizationParams) -> str:
-    axis = "null" if p.axis is None else str(int(p.axis))
-    return (f'{{"bits":{int(p.bits)},"scale":{_json_f32(p.scale)},"zero_point":{int(p.zero_point)},'
-            f'"symmetric":{"true" if p.symmetric else "false"},"axis":{axis}}}')
+    """``bincode::deserialize`` (trailing bytes allowed, bincode 1.3 legacy options) or, with
+    ``strict``, the DefaultOptions reader that rejects them."""
+    q = _QP()
+    check(_lib.load().dllm_qparams_from_bincode(bytes(b), len(b), int(strict), C.byref(q), None))
+    return _params(q)
 
 
 def params_to_json(p: QuantizationParams) -> str:
-    return _params_json(p)
-
-
-def _params_from_obj(o) -> QuantizationParams:
-    scale = F32(float("nan") if o["scale"] is None else float(o["scale"]))
-    return QuantizationParams(bits=int(o["bits"]), scale=float(scale), zero_point=int(o["zero_point"]),
-                              symmetric=bool(o["symmetric"]), axis=None if o["axis"] is None else int(o["axis"]))
+    q = _qp(p)
+    return _emit(_lib.load().dllm_qparams_to_json, C.byref(q)).decode()
 
 
 def params_from_json(s: str) -> QuantizationParams:
-    return _params_from_obj(json.loads(s))
+    b = s.encode()
+    q = _QP()
+    check(_lib.load().dllm_qparams_from_json(b, len(b), C.byref(q)))
+    return _params(q)
 
 
 # ---- QuantizedTensor (quantization crate) -------------------------------------------------------------
 
 def _host_codes(t: QuantizedTensor) -> np.ndarray:
     d = t.data
-    return d.detach().to("cpu").numpy().astype(np.uint8).ravel() if isinstance(d, torch.Tensor) else \
-        np.asarray(d, np.uint8).ravel()
+    return _u8(d.detach().to("cpu").numpy() if isinstance(d, torch.Tensor) else d)
 
 
 def qtensor_to_bincode(t: QuantizedTensor) -> bytes:
-    return _b_bytes(_host_codes(t)) + _b_usize_vec(t.shape) + _b_params(t.params)
-
-
-def qtensor_from_bincode(b: bytes, device="cuda", strict: bool = False) -> QuantizedTensor:
-    r = _Reader(b, strict)
-    data, shape = r.bytes_vec(), r.usize_vec()
-    params = _r_params(r)
-    r.done()
-    return QuantizedTensor(torch.from_numpy(data).to(device), tuple(shape), params)
+    codes, q = _host_codes(t), _qp(t.params)
+    return _emit(_lib.load().dllm_qtensor_to_bincode, codes.ctypes.data, codes.size, _shape(t.shape), len(t.shape),
+                 C.byref(q))
 
 
 def qtensor_to_json(t: QuantizedTensor) -> str:
-    shape = "[" + ",".join(str(int(s)) for s in t.shape) + "]"
-    return f'{{"data":{_json_u8_array(_host_codes(t))},"shape":{shape},"params":{_params_json(t.params)}}}'
+    codes, q = _host_codes(t), _qp(t.params)
+    return _emit(_lib.load().dllm_qtensor_to_json, codes.ctypes.data, codes.size, _shape(t.shape), len(t.shape),
+                 C.byref(q)).decode()
 
 
-def _u8_array(v) -> np.ndarray:
-    """serde's Vec<u8> visitor: every element an integer in 0..=255, else a data error."""
-    if not isinstance(v, list) or not all(type(e) is int and 0 <= e <= 255 for e in v):
-        raise _lib.SerializationError("json: data must be an array of integers in 0..=255")
-    return np.asarray(v, dtype=np.uint8)
+def _decode_tensor(fn, buf, extra, device) -> QuantizedTensor:
+    n, nd, q = C.c_size_t(), C.c_size_t(), _QP()
+    check(fn(buf, len(buf), *extra, None, 0, C.byref(n), None, 0, C.byref(nd), C.byref(q)))   # counts
+    codes = np.zeros(max(1, n.value), np.uint8)
+    shape = (C.c_uint64 * max(1, nd.value))()
+    check(fn(buf, len(buf), *extra, codes.ctypes.data, codes.size, C.byref(n), shape, len(shape), C.byref(nd),
+             C.byref(q)))
+    return QuantizedTensor(torch.from_numpy(codes[: n.value].copy()).to(device), tuple(int(v) for v in shape[: nd.value]),
+                           _params(q))
+
+
+def qtensor_from_bincode(b: bytes, device="cuda", strict: bool = False) -> QuantizedTensor:
+    return _decode_tensor(_lib.load().dllm_qtensor_from_bincode, bytes(b), (int(strict),), device)
 
 
 def qtensor_from_json(s: str, device="cuda") -> QuantizedTensor:
-    o = json.loads(s)
-    return QuantizedTensor(torch.from_numpy(_u8_array(o["data"])).to(device), tuple(int(v) for v in o["shape"]),
-                           _params_from_obj(o["params"]))
+    return _decode_tensor(_lib.load().dllm_qtensor_from_json, s.encode(), (), device)
 
 
 # ---- diffusion_prefill CompressedVector ------------------------------------------------------------------
@@ -232,34 +142,40 @@ class PrefillCompressedVector:
     quant_scale: float
     quant_zero_point: float
 
+    def _args(self):
+        idb, d = self.id.encode("utf-8"), _u8(self.data)
+        return (idb, len(idb), d.ctypes.data, d.size, int(self.bits), _shape(self.original_shape),
+                len(self.original_shape), C.c_float(self.quant_scale), C.c_float(self.quant_zero_point)), d
+
     def to_bincode(self) -> bytes:
-        idb = self.id.encode("utf-8")
-        return (struct.pack("<Q", len(idb)) + idb + _b_bytes(self.data) + struct.pack("<B", int(self.bits)) +
-                _b_usize_vec(self.original_shape) + struct.pack("<ff", float(F32(self.quant_scale)),
-                                                                float(F32(self.quant_zero_point))))
+        args, _keep = self._args()
+        return _emit(_lib.load().dllm_compressed_vector_to_bincode, *args)
+
+    def to_json(self) -> str:
+        args, _keep = self._args()
+        return _emit(_lib.load().dllm_compressed_vector_to_json, *args).decode()
+
+    @classmethod
+    def _decode(cls, fn, buf: bytes, extra) -> "PrefillCompressedVector":
+        il, n, nb, nd, sc, zp = C.c_size_t(), C.c_size_t(), C.c_uint8(), C.c_size_t(), C.c_float(), C.c_float()
+        tail = (C.byref(nb),)
+        check(fn(buf, len(buf), *extra, None, 0, C.byref(il), None, 0, C.byref(n), *tail, None, 0, C.byref(nd),
+                 C.byref(sc), C.byref(zp)))
+        ib = C.create_string_buffer(max(1, il.value))
+        data = np.zeros(max(1, n.value), np.uint8)
+        shape = (C.c_uint64 * max(1, nd.value))()
+        check(fn(buf, len(buf), *extra, ib, len(ib), C.byref(il), data.ctypes.data, data.size, C.byref(n), *tail,
+                 shape, len(shape), C.byref(nd), C.byref(sc), C.byref(zp)))
+        return cls(ib.raw[: il.value].decode("utf-8"), data[: n.value].copy(), int(nb.value),
+                   [int(v) for v in shape[: nd.value]], float(np.float32(sc.value)), float(np.float32(zp.value)))
 
     @classmethod
     def from_bincode(cls, b: bytes, strict: bool = False) -> "PrefillCompressedVector":
-        r = _Reader(b, strict)
-        v = cls(r.string(), r.bytes_vec(), r.u8(), r.usize_vec(), float(r.f32()), float(r.f32()))
-        r.done()
-        return v
-
-    def to_json(self) -> str:
-        shape = "[" + ",".join(str(int(s)) for s in self.original_shape) + "]"
-        return (f'{{"id":{json.dumps(self.id, ensure_ascii=False)},"data":{_json_u8_array(self.data)},'
-                f'"bits":{int(self.bits)},"original_shape":{shape},"quant_scale":{_json_f32(self.quant_scale)},'
-                f'"quant_zero_point":{_json_f32(self.quant_zero_point)}}}')
+        return cls._decode(_lib.load().dllm_compressed_vector_from_bincode, bytes(b), (int(strict),))
 
     @classmethod
     def from_json(cls, s: str) -> "PrefillCompressedVector":
-        o = json.loads(s)
-        f = (lambda v: float(F32(float("nan") if v is None else float(v))))
-        bits = int(o["bits"])
-        if not 0 <= bits <= 255:
-            raise _lib.SerializationError("json: bits out of u8 range")
-        return cls(o["id"], _u8_array(o["data"]), bits, [int(v) for v in o["original_shape"]],
-                   f(o["quant_scale"]), f(o["quant_zero_point"]))
+        return cls._decode(_lib.load().dllm_compressed_vector_from_json, s.encode("utf-8"), ())
 
 
 def compressed_vector_records(x: torch.Tensor, bits: int, ids: Optional[List[str]] = None) -> List[PrefillCompressedVector]:

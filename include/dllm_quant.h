@@ -94,6 +94,11 @@ int dllm_tensor_extremes(const float *x, size_t n, float *stats, void *workspace
 int dllm_quantize_params_from_extremes(const float *stats, uint8_t bits, float *params, dllm_stream_t stream);
 int dllm_quantize_tensor_with_params(const float *x, size_t n, uint8_t bits, int packed, const float *params,
                                      uint8_t *out, dllm_stream_t stream);
+/* The same at two widths in one read of x (KVCacheEntry::update's prefill and decode copies of a
+ * head shard, diffuse-llm-rs/src/lib.rs:246-276); == two dllm_quantize_tensor_with_params calls. */
+int dllm_quantize_tensor_pair_with_params(const float *x, size_t n, uint8_t bits_a, uint8_t bits_b, int packed,
+                                          const float *params_a, const float *params_b, uint8_t *out_a,
+                                          uint8_t *out_b, dllm_stream_t stream);
 
 /* dequantize_tensor(data: &[u8], scale: f32, zero_point: f32) -> Vec<f32> (quantization.rs:81-85)
  * and QuantizedTensor::dequantize (:115-117):  y = ((q as f32) - zp) * scale.
@@ -195,7 +200,11 @@ enum dllm_precision { DLLM_PRECISION_EXACT = 0, DLLM_PRECISION_F16W = 1 };
 
 /* W (device, f32 [K][N] row-major), bias (device f32 [N] or NULL = zeros, the reference's
  * Array1::zeros, lib.rs:798).  Quantization runs on the GPU (bit-exact with a1).  Precision
- * DLLM_PRECISION_EXACT. */
+ * DLLM_PRECISION_EXACT.  Create builds everything a forward reads -- the prefill and decode code
+ * layouts, the per-(group, column) parameters and, for int4 g128 EXACT handles with N % 256 == 0,
+ * the Horner-form ratios s_{g-1}/s_g with the check that the scales allow that form -- in
+ * temporaries of its own, and synchronises `stream` once before it returns (it is not capturable).
+ * The handle is immutable afterwards: safe to share across threads on distinct streams. */
 int dllm_linear_create(const float *W, const float *bias, size_t K, size_t N, uint8_t bits, size_t group,
                        dllm_linear_t *out, dllm_stream_t stream);
 int dllm_linear_create_ex(const float *W, const float *bias, size_t K, size_t N, uint8_t bits, size_t group,
@@ -212,13 +221,12 @@ int dllm_linear_create_quantized_ex(const uint8_t *packed_codes, const float *sc
  * through a workspace owned by the handle.  Shapes with too few output tiles to fill the GPU
  * (M roughly 65..1000 at N = 4096) split K into slices whose f32 partials are combined in slice
  * order (deterministic) through a per-(device, stream) workspace.  Both workspaces only grow and
- * are allocated on the first call that needs them, which therefore must precede stream capture;
- * likewise the decode-fragment copy of the weights, built by the handle's first M <= 64 call
- * (a capture-time first call returns DLLM_ERR_INVALID_PARAMS).  DLLM_PRECISION_EXACT, int4 g128,
- * on grids of >= 256 tiles of 256 x 256 (M >= 4096 at N = 4096): the handle's first such call
- * builds the Horner-form ratios s_{g-1}/s_g (one synchronisation, [G + 1][N] f32) and checks that
- * the scales allow that form; inside stream capture it does not, and the call runs the fold-form
- * kernel instead (same bound, different f32 summation order). */
+ * are allocated on the first call that needs them, which therefore must precede stream capture.
+ * Otherwise the call only launches kernels on `stream`: it never synchronises, and the kernel a
+ * shape runs (hence its result bits) does not depend on call history or on capture.
+ * DLLM_PRECISION_EXACT, int4 g128, on grids of >= 256 tiles of 256 x 256 (M >= 4096 at N = 4096)
+ * runs the Horner-form kernel when the handle's create accepted its ratios, else the fold form
+ * (same bound, different f32 summation order). */
 int dllm_linear_forward(dllm_linear_t h, const void *X, size_t M, int x_dtype, void *Y, int y_dtype,
                         dllm_stream_t stream);
 /* Export the quantized weights in canonical form (packed bitstream [K][N], scales [G][N], zps);
@@ -229,10 +237,9 @@ int dllm_linear_info(dllm_linear_t h, size_t *K, size_t *N, uint8_t *bits, size_
 int dllm_linear_precision(dllm_linear_t h);   /* DLLM_PRECISION_*, -1 on a null handle */
 /* HBM bytes the forward's GEMM kernel reads for the weights (packed codes + scales/zps). */
 size_t dllm_linear_weight_bytes(dllm_linear_t h);
-/* Device memory the handle owns: the prefill code layout and the per-(group, column) parameters
- * (f16 zero-point/scale pairs + f32 scales) -- 9.02 MiB at 4096 x 4096 int4 g128 -- plus, once
- * built, the decode code layout (+8 MiB there), the Horner ratios (+0.52 MiB there) and the X
- * staging workspace once grown. */
+/* Device memory the handle owns: the prefill and decode code layouts and the per-(group, column)
+ * parameters (f16 zero-point/scale pairs + f32 scales) -- 17.02 MiB at 4096 x 4096 int4 g128 --
+ * plus the Horner ratios where kept (+0.52 MiB there) and the X staging workspace once grown. */
 size_t dllm_linear_device_bytes(dllm_linear_t h);
 #ifdef DLLM_LAB
 /* Lab build only (libdllm_hip_lab.so): A/B schedule variants and ablation masks; mutates the
@@ -284,6 +291,9 @@ int dllm_compressed_vector_from_bincode(const uint8_t *buf, size_t len, int stri
 int dllm_compressed_vector_to_json(const char *id, size_t id_len, const uint8_t *data, size_t n, uint8_t bits,
                                    const uint64_t *shape, size_t ndim, float scale, float zero_point, char *out,
                                    size_t cap, size_t *len);
+int dllm_compressed_vector_from_json(const char *s, size_t len, char *id, size_t id_cap, size_t *id_len,
+                                     uint8_t *data, size_t data_cap, size_t *n, uint8_t *bits, uint64_t *shape,
+                                     size_t shape_cap, size_t *ndim, float *scale, float *zero_point);
 
 /* ---- a9: int-quantized KV dequant-attention (consumer of QuantizedKVCacheEntry) -------------
  * The reference dequantizes K/V (QuantizedKVCacheEntry::dequantize_keys/values,

@@ -6,5 +6,5 @@ export TMPDIR=/tmp
 OUT="$PWD/gpurun_out/quant_ab"
 mkdir -p "$OUT"
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/fused" -o qp --output-format csv -- python3 scripts/quant_probe.py 20 > "$OUT/fused.log" 2>&1 || exit $?
-DLLM_QUANT_GENERIC=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/generic" -o qp --output-format csv -- python3 scripts/quant_probe.py 20 > "$OUT/generic.log" 2>&1 || exit $?
+DLLM_LIB=lab DLLM_QUANT_GENERIC=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/generic" -o qp --output-format csv -- python3 scripts/quant_probe.py 20 > "$OUT/generic.log" 2>&1 || exit $?
 echo done

@@ -31,6 +31,18 @@ def test_header_symbols_exported(dllm):
         assert not hasattr(lib, s), f"{s} is lab-only but the product library exports it"
 
 
+def test_product_library_has_no_lab_switches(dllm):
+    """The product library reads no environment on its compute paths: the A/B schedules and ablation
+    masks (DLLM_ATTN_LAB, DLLM_LAB_HORNER128, ...) exist only in the lab build."""
+    so = dllm._lib.LIB_PATH.read_bytes()
+    for knob in (b"DLLM_ATTN_LAB", b"DLLM_LAB_HORNER128", b"DLLM_QUANT_GENERIC"):
+        assert knob not in so, knob
+    import subprocess
+    undef = subprocess.run(["nm", "-D", "--undefined-only", str(dllm._lib.LIB_PATH)], capture_output=True,
+                           text=True).stdout.split()
+    assert "getenv" not in undef and "getenv@GLIBC_2.2.5" not in undef, "the product library calls getenv"
+
+
 def test_library_is_gfx950(dllm):
     so = dllm._lib.LIB_PATH.read_bytes()
     assert b"gfx950" in so, "libdllm_hip.so carries no gfx950 code object"

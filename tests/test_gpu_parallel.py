@@ -147,3 +147,89 @@ def test_bench_column_shard_random_vs_f32(dllm, torch, orc, G):
         ref = X.float() @ _dequantized(col.local, orc)
         assert _rel(Y.float(), ref) <= REL_TOL, (r, _rel(Y.float(), ref))
         col.local.close()
+
+
+def _unpacked(dllm, q):
+    """One code per byte of a packed QuantizedTensor, reshaped to its tensor shape (GPU unpack)."""
+    return dllm.unpack(q.data, q.numel(), q.bits).reshape(q.shape)
+
+
+@pytest.mark.parametrize("G", [2, 4, 8])
+def test_denoise_loop_config5_sharded(dllm, torch, orc, G):
+    """Config C5 sharded as a whole loop (SURVEY.md 8e; DiffuseLLM::sample, diffuse-llm-rs/src/lib.rs:
+    853-955): 12 int4 g128 layers of d 4096 as 6 hidden-dim-sharded Megatron pairs, seq 2048, 50
+    steps, with the phase-aware KV cache (8 / 4 bits, progressive precision on, lib.rs:121-313,
+    884-918) sharded by head (32 heads of 128) -- G ranks emulated in one process
+    (parallel.EmulatedTensorParallel: the pair's f32 partials summed in rank order;
+    parallel.EmulatedHeadParallelKV: one max of the shards' K/V extremes per quantization), against
+    the unsharded loop (QuantLinear layers, KVCacheEntry) and the f32 chain.  Teacher-forced: every
+    step maps the sharded run's own x_t through (a) the sharded step, (b) the unsharded step, (c) the
+    reference in f32 (x.dot(W) per layer on the oracle-dequantized weights, lib.rs:806-813, then
+    p_sample with the same noise).  At every step:
+      * (a) vs (c) <= 1e-3 relative (BASELINE.md's C5 bar);
+      * (a) vs (b) <= 1e-4: the same arithmetic but for the f32 order of the partial sums (and the
+        rare f16 tie of a hidden activation that order flips);
+      * phase, decode width, and every shard's codes and params of both cached copies bit-identical
+        to the unsharded cache's for the shard's heads.
+    The per-step errors go to gpurun_out/c5_sharded_G{G}.json."""
+    import json
+    import os
+    par = dllm.parallel
+    d, M, L, steps, seed, heads = 4096, 2048, 12, 50, 7, 32
+    g = torch.Generator(device="cuda").manual_seed(7)
+    Ws = [(1.0 / 64.0) * torch.randn(d, d, device="cuda", generator=g) for _ in range(L)]
+    cfg = dllm.DiffusionConfig(num_timesteps=steps, hidden_size=d, num_layers=L, num_attention_heads=heads)
+    K = torch.randn(1, M, d, device="cuda", generator=g)
+    V = 0.5 * torch.randn(1, M, d, device="cuda", generator=g)
+    x = torch.randn(M, d, device="cuda", generator=g)
+    unsh = [dllm.QuantLinear.from_weight(W, None, 4, 128) for W in Ws]
+    Wh = [_dequantized(lin, orc) for lin in unsh]
+    pairs = [par.EmulatedTensorParallel([par.TensorParallelPair(Ws[2 * p], None, Ws[2 * p + 1], None, 4, 128,
+                                                                shard=(G, r)) for r in range(G)])
+             for p in range(L // 2)]
+    kv_u = dllm.KVCacheEntry.new(K, V, cfg.prefill_bits, cfg.decode_bits)
+    kv_s = par.EmulatedHeadParallelKV(K, V, cfg.prefill_bits, cfg.decode_bits, heads, G)
+    loop_u = dllm.DenoiseLoop(unsh, cfg, cumprod=dllm.Cumprod.INCLUSIVE, seed=seed, kv_cache=kv_u, overlap=False)
+    loop_s = dllm.DenoiseLoop(pairs, cfg, cumprod=dllm.Cumprod.INCLUSIVE, seed=seed, kv_cache=kv_s, overlap=False)
+    errs, errs_u, widths = [], [], []
+    for i, t in enumerate(range(steps - 1, -1, -1)):
+        loop_u.kv_step(t, steps)
+        loop_s.kv_step(t, steps)
+        assert kv_s.is_prefill_phase == kv_u.is_prefill_phase and kv_s.decode_quant_bits == kv_u.decode_quant_bits
+        widths.append(kv_u.get_current_quant_bits())
+        for qu, qs in ((kv_u.prefill_quantized, kv_s.prefill_quantized), (kv_u.decode_quantized, kv_s.decode_quantized)):
+            assert (qu is None) == (qs is None), i
+            if qu is None:
+                continue
+            for which in ("keys", "values"):
+                full = _unpacked(dllm, getattr(qu, which))
+                pu = getattr(qu, which).params.view(torch.int32)
+                for (c0, c1), sh in zip(kv_s.cols, qs):
+                    part = getattr(sh, which)
+                    assert torch.equal(_unpacked(dllm, part), full[..., c0:c1]), (i, which, c0)
+                    assert torch.equal(part.params.view(torch.int32), pu), (i, which, c0)
+        xs = loop_s.step(x, t, i)
+        xu = loop_u.step(x, t, i)
+        coef, flag = dllm.diffusion.p_sample_coeffs(cfg, [t], 1, dllm.Cumprod.INCLUSIVE)
+        c1_, c2_, sd = (float(v) for v in coef[0])
+        nz = dllm.randn(M * d, seed, i * M * d).reshape(M, d) if flag else 0.0
+        h = x
+        for W in Wh:
+            h = h @ W
+        ref = (c1_ * x + c2_ * h) + sd * nz
+        errs.append(_rel(xs, ref))
+        errs_u.append(_rel(xs, xu))
+        x = xs
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open(f"gpurun_out/c5_sharded_G{G}.json", "w") as f:
+        json.dump({"G": G, "rel_err_vs_f32_chain": errs, "rel_diff_vs_unsharded_step": errs_u,
+                   "max": max(errs), "max_vs_unsharded": max(errs_u), "widths": widths}, f)
+    print(f"C5 sharded G={G}: max rel err vs f32 chain {max(errs):.3e}, vs unsharded step {max(errs_u):.3e}")
+    assert bool(torch.isfinite(x).all())
+    assert max(errs) <= REL_TOL, max(errs)
+    assert max(errs_u) <= 1e-4, max(errs_u)
+    assert widths == [8] * 24 + [2] + [1] * 12 + [0] * 13
+    for lin in unsh:
+        lin.close()
+    for p in pairs:
+        p.close()
