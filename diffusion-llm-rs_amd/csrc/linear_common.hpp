@@ -246,6 +246,21 @@ struct ExactGemmArgs {
     const float *hr = nullptr;   // Horner ratios (DLLM_EXACT_HORNER builds: the 128 x 256 tiles in Horner form)
 };
 int launch_exact_gemm(const ExactGemmArgs &a, int y_f32, hipStream_t st);
+
+// Exact-weight int4 g128 GEMM in Horner form on 256 x 256 tiles (linear_horner.hip): hr = the
+// handle's ratios [G + 1][Npad], sf = its f32 scales (the last group's multiply the result).
+// Needs K % 128 == 0 and Npad % 256 == 0.
+struct HornerGemmArgs {
+    const __half *X;
+    int M, K;
+    const uint32_t *wdev, *sz;
+    const float *hr, *sf, *bias;
+    void *Y;
+    int N, Npad;
+    const PSampleEpi *epi;
+    int lab = 0;   // lab build only: 1 = the unstaggered schedule (A/B); 2 / 3 = staggered / not, no stores
+};
+int launch_horner_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st);
 bool exact_gemm_supported(int M, int K, int Npad, int group);
 
 // Ping-pong 256 x 256 GEMM (linear_pp.hip): Y = X . W^ + b for the 256-column-tile grid, bits in

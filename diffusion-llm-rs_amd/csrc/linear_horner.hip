@@ -1,0 +1,362 @@
+// linear_horner.hip -- the exact-weight int4 g128 GEMM in Horner form on 256 x 256 tiles: the
+// default kernel of the headline shape (M = K = N = 4096) and of every int4 g128 layer whose
+// 256 x 256 grid fills the chip.
+//
+// Replaces SimpleDiffusionModel::forward = x.dot(W) + b (diffuse-llm-rs/src/lib.rs:806-813) with
+// W quantized per (column n, 128-row group g) by quantize_tensor (quantization.rs:38-68); the
+// weight is the reference's f32 a2 value (q - zp) * s (quantization.rs:81-85): the MFMA A operand
+// is the exact integer q - zp (f16) and the f32 group scale enters in Horner form,
+//   acc <- acc * r_g + T_g,  r_g = s_{g-1} / s_g (hr[g][n], r_0 = 1),  T_g = sum_{k in g} X (q - zp),
+// so after the last group acc = sum_g T_g s_g / s_{G-1} and the epilogue multiplies by s_{G-1}.
+// The handle's create checks that every column's scales allow the form (linear_wq.hip).
+//
+// Structure (Y^T = W^T X^T: the accumulator's lane is the token, 4 consecutive registers are 4
+// consecutive columns): block 256 tokens x 256 columns, 8 waves side by side in n (2 per SIMD),
+// wave tile 32 columns x 256 tokens (acc = 8 x 16 f32).  Per 64-deep k-step a stage holds the X
+// tile (32 KiB, XOR-swizzled 16-B chunks), the 8 waves' weight words (8 KiB) and, on a group's
+// first k-step, the group's {zp, scale} pairs and ratios (2 KiB); 3 stages in a ring, stage kt+2
+// issued while kt computes, one counted vmcnt wait and one raw s_barrier per k-step.
+//
+// Against wq_gemm8_kernel<..., HORNER> (linear_wq.hip, the same arithmetic and schedule, bit for bit)
+// this kernel cuts the instruction stream around the MFMAs, which two waves per SIMD must share:
+//   * a stage is ONE inline-asm burst per wave: buffer_load_dwordx4 ... lds with fixed per-lane
+//     VGPR offsets and the k-step in an SGPR offset, M0 stepped by s_add between the DMAs (the LDS
+//     destinations of a wave's X pieces and its weight words are 8 KiB apart), saved/restored once
+//     per burst -- no per-DMA address VALU, no per-DMA M0 save/restore, no integer division;
+//   * the group's {zp, scale} and ratios travel only with its first stage, and the zero-point
+//     constants of dequant_exact are built once per group.
+#include "linear_common.hpp"
+
+#include <type_traits>
+
+#ifndef DLLM_LAB
+#define DLLM_LAB 0
+#endif
+
+namespace dllm {
+namespace {
+
+constexpr int kHX = 256 * kBK * 2;            // X tile bytes per stage (32 KiB)
+constexpr int kHW = 8 * 1024;                 // 8 waves x 64 lanes x 16 B of weight words
+constexpr int kHG = 2048;                     // sz (1 KiB) + ratios (1 KiB), group-first stages
+constexpr int kHStage = kHX + kHW + kHG;      // 43008 B; 3 stages = 126 KiB
+
+// One wave's stage burst: 4 X pieces (rows (8 i + wave) 8 ..) and its weight words, LDS-DMA
+// through buffer descriptors.  lds0 = this wave's first X destination; the next pieces follow at
+// +8 KiB (X piece i at wave * 1 KiB + i * 8 KiB, the weight words at 32 KiB + wave * 1 KiB).
+__device__ __forceinline__ void horner_burst(__amdgpu_buffer_rsrc_t xr, uint32_t x0, uint32_t x1, uint32_t x2,
+                                             uint32_t x3, uint32_t sx, __amdgpu_buffer_rsrc_t wr, uint32_t wo,
+                                             uint32_t sw, uint32_t lds0) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %9\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %5, %6 offen lds\n\t"
+        "s_add_u32 m0, m0, 0x2000\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %2, %5, %6 offen lds\n\t"
+        "s_add_u32 m0, m0, 0x2000\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %3, %5, %6 offen lds\n\t"
+        "s_add_u32 m0, m0, 0x2000\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %4, %5, %6 offen lds\n\t"
+        "s_add_u32 m0, m0, 0x2000\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %7, %8, %10 offen lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(x0), "v"(x1), "v"(x2), "v"(x3), "s"(xr), "s"(sx), "v"(wo), "s"(wr), "s"(lds0), "s"(sw)
+        : "memory");
+}
+
+// MODE bit 0: the staggered schedule (product); bit 1 (lab ablation only): no output stores.
+template <typename YT, int EPI, int MODE>
+__global__ void __launch_bounds__(512, 1)
+wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdev,
+                 const uint32_t *__restrict__ sz, const float *__restrict__ hr, const float *__restrict__ sf,
+                 const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad, int nbm, int nbn,
+                 PSampleEpi epi) {
+    constexpr bool STAG = MODE & 1;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[3 * kHStage];
+
+    // XCD-aware bijective remap: blocks b and b + 8 share an XCD under round-robin dispatch, so the
+    // 32 tiles an XCD holds at once are consecutive (2 row-blocks x 16 column-blocks at N = 4096).
+    const int nb = nbm * nbn, orig = blockIdx.x;
+    const int xcd = orig % kXCDs, q8 = nb / kXCDs, r8 = nb % kXCDs;
+    const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / kXCDs;
+    const int bm = tile / nbn, bn = tile % nbn;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int m0 = bm * 256, n0 = bn * 256;
+    const int nk = K / kBK;   // 64-deep k-steps, even (K % 128 == 0)
+
+    // DMA sources: buffer descriptors at the block's first X row / the wave's weight column tile /
+    // the block's first column of sz and hr, fixed per-lane offsets, the k-step in the SGPR offset.
+    uint32_t xo[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int row = (i * 8 + wave) * 8 + (lane >> 3);
+        const int rrow = (m0 + row < M ? m0 + row : M - 1) - m0;   // rows past M re-read row M - 1
+        const int c = (lane & 7) ^ ((row >> 1) & 7);
+        xo[i] = static_cast<uint32_t>((rrow * K + c * 8) * 2);
+    }
+    const __amdgpu_buffer_rsrc_t xr = raw_rsrc(X + static_cast<size_t>(m0) * K);
+    const uint32_t nt = static_cast<uint32_t>(n0 + 32 * wave) >> 5;
+    const __amdgpu_buffer_rsrc_t wr = raw_rsrc(wdev + static_cast<size_t>(nt) * nk * 64 * 4);
+    const uint32_t wo = static_cast<uint32_t>(lane * 16);
+    // group data: wave 0 stages the {zp, scale} pairs, wave 1 the ratios (256 columns x 4 B each)
+    const __amdgpu_buffer_rsrc_t gr =
+        raw_rsrc(wave == 0 ? static_cast<const void *>(sz + n0) : static_cast<const void *>(hr + n0));
+    const bool has_g = wave < 2;
+    const uint32_t sbase = __builtin_amdgcn_readfirstlane(lds_addr(smem));
+
+    auto stage = [&](int slot, int kt, bool gf) __attribute__((always_inline)) {
+        const uint32_t base = sbase + static_cast<uint32_t>(slot * kHStage);
+        horner_burst(xr, xo[0], xo[1], xo[2], xo[3], static_cast<uint32_t>(kt * kBK * 2), wr, wo,
+                     static_cast<uint32_t>(kt * 1024), base + static_cast<uint32_t>(wave * 1024));
+        if (gf && has_g)
+            blds16_asm(gr, wo, static_cast<uint32_t>((kt >> 1) * Npad * 4),
+                       base + static_cast<uint32_t>(kHX + kHW + wave * 1024));
+    };
+
+    float16_t acc[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[r][e] = 0.0f;
+
+    const int hsel = lane >> 5;
+    const int rowx = ((lane & 31) >> 1) & 7;
+    int soff[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) soff[s] = (lane & 31) * (kBK * 2) + ((((2 * s + hsel) ^ rowx)) << 4);
+
+    auto read_b = [&](half8_t (&b)[8], const uint8_t *sb, int s) __attribute__((always_inline)) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) b[r] = *reinterpret_cast<const half8_t *>(sb + soff[s] + r * 32 * kBK * 2);
+    };
+
+    ExactConsts ec;
+    uint32_t w[4];
+    float4 r4[4];
+    half8_t bA[8], bB[8], aA, aB;
+    auto sub = [&](const uint8_t *sb, half8_t (&bc)[8], half8_t (&bn)[8], const half8_t &ac, half8_t &an, int j,
+                   bool gf) __attribute__((always_inline)) {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+        if (j < 3) {
+            read_b(bn, sb, j + 1);
+            an = dequant_exact<4>(w, j + 1, ec);
+        }
+        if (gf && j == 0) {
+            // acc <- acc * r_g right before the group's first MFMA of each rep (scalar v_mul_f32:
+            // the file is built without the SLP vectorizer)
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+#pragma unroll
+                for (int qd = 0; qd < 4; ++qd) {
+                    acc[r][4 * qd + 0] *= r4[qd].x;
+                    acc[r][4 * qd + 1] *= r4[qd].y;
+                    acc[r][4 * qd + 2] *= r4[qd].z;
+                    acc[r][4 * qd + 3] *= r4[qd].w;
+                }
+                acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bc[r], acc[r], 0, 0, 0);
+            }
+            // rep i + 1's rescale issues beside rep i's MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                if (i + 1 < 8) __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bc[r], acc[r], 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+            }
+        }
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto barrier = []() __attribute__((always_inline)) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // STAG (the default): waves 4-7 (the second of each SIMD's two waves) run half a k-step behind
+    // waves 0-3 -- one barrier per half k-step, group B entering through one extra barrier -- so a
+    // SIMD's two waves do not reach their LDS read bursts, dequant / rescale VALU and barrier waits
+    // together (MI355X_MICROARCH.md, two waves per SIMD, item 9).  Ring safety: stage kt + 2 is
+    // issued in the second half of k-step kt, after the barrier behind which the lagging group
+    // finished reading slot (kt - 1) % 3; a wave of group A waits for its stage kt + 1 DMAs at the
+    // end of that half (they were issued a half k-step earlier than group B's), a wave of group B at
+    // the end of the first half of k-step kt + 1 (vmcnt 0), in both cases before the barrier behind
+    // which the first wave reads stage kt + 1.
+    const bool grp_b = STAG && wave >= 4;
+    // One k-step on ring slot `slot` (k-step kt); slot (kt + 2) % 3 receives k-step kt + 2.
+    auto step = [&](int slot, int kt, auto gf_tag) __attribute__((always_inline)) {
+        constexpr bool GF = decltype(gf_tag)::value;
+        const bool issue = kt + 2 < nk;
+        if (!STAG && issue) stage((slot + 2) % 3, kt + 2, GF);   // kt + 2 opens a group iff kt does
+        const uint8_t *sb = smem + slot * kHStage;
+        {
+            const uint4 v = *reinterpret_cast<const uint4 *>(sb + kHX + wave * 1024 + lane * 16);
+            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+        }
+        if constexpr (GF) {
+            half2_t nz, sc;
+            split_sz(*reinterpret_cast<const uint32_t *>(sb + kHX + kHW + (wave * 32 + (lane & 31)) * 4), nz, sc);
+            ec = exact_consts(nz);
+            const float *rl = reinterpret_cast<const float *>(sb + kHX + kHW + 1024) + wave * 32 + 4 * hsel;
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd) r4[qd] = *reinterpret_cast<const float4 *>(rl + 8 * qd);
+        }
+        read_b(bA, sb, 0);
+        aA = dequant_exact<4>(w, 0, ec);
+        sub(sb, bA, bB, aA, aB, 0, GF);
+        sub(sb, bB, bA, aB, aA, 1, GF);
+        if constexpr (STAG) {
+            if (grp_b) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            barrier();
+            if (issue) stage((slot + 2) % 3, kt + 2, GF);
+        }
+        sub(sb, bA, bB, aA, aB, 2, GF);
+        sub(sb, bB, bA, aB, aA, 3, GF);
+        // k-step kt + 1 must have landed; kt + 2's DMAs stay in flight across the barrier
+        if (!grp_b) {
+            if (issue) {
+                if (GF && has_g) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        }
+        barrier();
+    };
+
+    stage(0, 0, true);
+    stage(1, 1, false);
+    asm volatile("s_waitcnt vmcnt(5)" ::: "memory");   // stage 0 landed (stage 1's 5 DMAs in flight)
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (grp_b) barrier();   // group B enters half a k-step behind
+    using GFt = std::integral_constant<bool, true>;
+    using GFf = std::integral_constant<bool, false>;
+    // group = 2 k-steps, ring period 3: unroll 6 so each step's slot and group phase are static
+    for (int kt = 0; kt < nk; kt += 6) {
+        step(0, kt, GFt{});
+        step(1, kt + 1, GFf{});
+        if (kt + 2 < nk) {
+            step(2, kt + 2, GFt{});
+            step(0, kt + 3, GFf{});
+        }
+        if (kt + 4 < nk) {
+            step(1, kt + 4, GFt{});
+            step(2, kt + 5, GFf{});
+        }
+    }
+    if (STAG && !grp_b) barrier();   // group A joins group B's last barrier
+
+    // acc = sum_g T_g s_g / s_{G-1}: times the last group's scales, then the bias
+    const int nb0 = n0 + wave * 32 + 4 * hsel;
+    const float *sl = sf + static_cast<size_t>(nk / 2 - 1) * Npad + nb0;
+    float4 bv[4];
+#pragma unroll
+    for (int qd = 0; qd < 4; ++qd) {
+        const float4 s = *reinterpret_cast<const float4 *>(sl + 8 * qd);
+        bv[qd] = *reinterpret_cast<const float4 *>(bias + nb0 + 8 * qd);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            acc[r][4 * qd + 0] *= s.x;
+            acc[r][4 * qd + 1] *= s.y;
+            acc[r][4 * qd + 2] *= s.z;
+            acc[r][4 * qd + 3] *= s.w;
+        }
+    }
+    if constexpr ((MODE & 2) != 0) {   // lab ablation: keep the results live, store nothing
+#pragma unroll
+        for (int r = 0; r < 8; ++r) asm volatile("" ::"v"(acc[r]));
+        return;
+    }
+    if constexpr (EPI == 1) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const int m = m0 + r * 32 + (lane & 31);
+            if (m >= M) continue;
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd) {
+                if (nb0 + 8 * qd >= N) continue;
+                psample4(epi, m, nb0 + 8 * qd, N, acc[r][4 * qd + 0] + bv[qd].x, acc[r][4 * qd + 1] + bv[qd].y,
+                         acc[r][4 * qd + 2] + bv[qd].z, acc[r][4 * qd + 3] + bv[qd].w);
+            }
+        }
+        return;
+    }
+    const bool full = (m0 + 256 <= M) && (n0 + 256 <= N) && (N % 4) == 0;
+    if (full) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            YT *yrow = Y + static_cast<size_t>(m0 + r * 32 + (lane & 31)) * N + nb0;
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd)
+                store4<YT>(yrow + 8 * qd, acc[r][4 * qd + 0] + bv[qd].x, acc[r][4 * qd + 1] + bv[qd].y,
+                           acc[r][4 * qd + 2] + bv[qd].z, acc[r][4 * qd + 3] + bv[qd].w);
+        }
+    } else {
+        const bool vec_ok = (N % 4) == 0;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const int m = m0 + r * 32 + (lane & 31);
+            if (m >= M) continue;
+            YT *yrow = Y + static_cast<size_t>(m) * N;
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd)
+                store_out4<YT>(yrow, bias, nb0 + 8 * qd, N, vec_ok, acc[r][4 * qd + 0], acc[r][4 * qd + 1],
+                               acc[r][4 * qd + 2], acc[r][4 * qd + 3]);
+        }
+    }
+}
+
+
+template <int MODE>
+void launch_horner_t(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
+    const int nbm = (a.M + 255) / 256, nbn = a.Npad / 256;
+    const unsigned nb = static_cast<unsigned>(nbm * nbn);
+    const PSampleEpi ep = a.epi ? *a.epi : PSampleEpi{};
+    if (a.epi)
+        wq_horner_kernel<float, 1, MODE><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
+                                                             a.epi->x_prev, a.N, a.Npad, nbm, nbn, ep);
+    else if (y_f32)
+        wq_horner_kernel<float, 0, MODE><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
+                                                             static_cast<float *>(a.Y), a.N, a.Npad, nbm, nbn, ep);
+    else
+        wq_horner_kernel<__half, 0, MODE><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
+                                                              static_cast<__half *>(a.Y), a.N, a.Npad, nbm, nbn, ep);
+}
+
+}  // namespace
+
+int launch_horner_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
+#if DLLM_LAB
+    if (a.lab == 1 || a.lab == 2 || a.lab == 3) {   // lab A/B: 1 no stagger; 2 / 3: + no stores (ablation)
+        if (a.lab == 1) launch_horner_t<0>(a, y_f32, st);
+        else if (a.lab == 2) launch_horner_t<3>(a, y_f32, st);
+        else launch_horner_t<2>(a, y_f32, st);
+        DLLM_LAUNCH_CHECK();
+        return DLLM_OK;
+    }
+#endif
+    launch_horner_t<1>(a, y_f32, st);
+    DLLM_LAUNCH_CHECK();
+    return DLLM_OK;
+}
+
+}  // namespace dllm

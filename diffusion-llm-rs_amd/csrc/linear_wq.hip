@@ -1915,8 +1915,8 @@ bool horner_ready(const dllm_linear *hc, int M, hipStream_t st) {
 
 template <typename YT, int EPI>
 int launch_horner(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t st, const PSampleEpi *epi) {
-    const PSampleEpi ep = epi ? *epi : PSampleEpi{};
 #if DLLM_LAB
+    const PSampleEpi ep = epi ? *epi : PSampleEpi{};
     if (lab_horner128()) {
         const int nbm = (M + 127) / 128, nbn = static_cast<int>(h->Npad / 256);
         wq_gemm8_kernel<4, YT, 8, 4, false, 1, 0, EPI, true><<<static_cast<unsigned>(nbm * nbn), 512, 0, st>>>(
@@ -1925,13 +1925,20 @@ int launch_horner(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream
         DLLM_LAUNCH_CHECK();
         return DLLM_OK;
     }
+    if (h->variant == 24) {   // lab A/B: the round-2 Horner kernel (wq_gemm8_kernel<..., HORNER>)
+        const int nbm = (M + 255) / 256, nbn = static_cast<int>(h->Npad / 256);
+        wq_gemm8_kernel<4, YT, 8, 8, false, 1, 0, EPI, true><<<static_cast<unsigned>(nbm * nbn), 512, 0, st>>>(
+            X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn, 1, nullptr,
+            ep, h->hr, h->sf);
+        DLLM_LAUNCH_CHECK();
+        return DLLM_OK;
+    }
 #endif
-    const int nbm = (M + 255) / 256, nbn = static_cast<int>(h->Npad / 256);
-    wq_gemm8_kernel<4, YT, 8, 8, false, 1, 0, EPI, true><<<static_cast<unsigned>(nbm * nbn), 512, 0, st>>>(
-        X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn, 1, nullptr, ep,
-        h->hr, h->sf);
-    DLLM_LAUNCH_CHECK();
-    return DLLM_OK;
+    HornerGemmArgs a{X, M, (int)h->K, h->wdev, h->sz, h->hr, h->sf, h->bias, Y, (int)h->N, (int)h->Npad, epi};
+#if DLLM_LAB
+    if (h->variant >= 25 && h->variant <= 27) a.lab = h->variant - 24;   // lab A/B (see HornerGemmArgs::lab)
+#endif
+    return launch_horner_gemm(a, std::is_same<YT, float>::value ? 1 : 0, st);
 }
 
 inline ExactGemmArgs exact_args(const dllm_linear *h, const __half *X, int M, void *Y, const PSampleEpi *epi) {
@@ -2341,8 +2348,8 @@ int dllm_linear_set_kernel_variant(dllm_linear_t h, int variant) {
         h->pplab = (variant - 100) % 32;
         return DLLM_OK;
     }
-    if (variant < -1 || variant > 15)
-        return fail(DLLM_ERR_INVALID_PARAMS, "variant must be -1..15 (16..23, 32..95, 100..195, 200..263: ablations)");
+    if (variant < -1 || (variant > 15 && (variant < 24 || variant > 27)))
+        return fail(DLLM_ERR_INVALID_PARAMS, "variant must be -1..15 or 24..27 (16..23, 32..95, 100..195, 200..263: ablations)");
     h->variant = variant;
     h->dlab = h->rlab = h->pplab = h->dcfg = 0;
     return DLLM_OK;
