@@ -301,6 +301,44 @@ wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
         return;
     }
     const bool full = (m0 + 256 <= M) && (n0 + 256 <= N) && (N % 4) == 0;
+    if constexpr (std::is_same<YT, __half>::value) {
+        if (full) {
+            // Coalesced f16 store through the (now idle) LDS ring, 128 token rows per pass: each
+            // wave writes its 32 columns of the pass's rows (8-B pieces, 16-B chunk index XORed
+            // with the row: conflict-free per 16-lane group), then every wave stores whole 512-B
+            // rows with 16-B lanes -- 1 KiB per instruction in 2 rows, instead of 64 rows x 8 B.
+            uint8_t *img = smem;
+            const int c0 = wave * 4;   // the wave's first 16-B chunk (8 columns each) of a row
+#pragma unroll
+            for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) {
+                    const int r = 4 * pass + rr;
+                    const int t = 32 * rr + (lane & 31);
+#pragma unroll
+                    for (int qd = 0; qd < 4; ++qd) {
+                        const int pc = (c0 + qd) ^ (t & 31);
+                        union { __half h[4]; uint2 u; } pk;
+                        pk.h[0] = __float2half_rn(acc[r][4 * qd + 0] + bv[qd].x);
+                        pk.h[1] = __float2half_rn(acc[r][4 * qd + 1] + bv[qd].y);
+                        pk.h[2] = __float2half_rn(acc[r][4 * qd + 2] + bv[qd].z);
+                        pk.h[3] = __float2half_rn(acc[r][4 * qd + 3] + bv[qd].w);
+                        *reinterpret_cast<uint2 *>(img + t * 512 + pc * 16 + hsel * 8) = pk.u;
+                    }
+                }
+                __syncthreads();
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const int t = 16 * wave + 2 * i + hsel;
+                    const int c = lane & 31;
+                    const uint4 v = *reinterpret_cast<const uint4 *>(img + t * 512 + ((c ^ (t & 31)) * 16));
+                    *reinterpret_cast<uint4 *>(Y + static_cast<size_t>(m0 + 128 * pass + t) * N + n0 + 8 * c) = v;
+                }
+                if (pass == 0) __syncthreads();
+            }
+            return;
+        }
+    }
     if (full) {
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
