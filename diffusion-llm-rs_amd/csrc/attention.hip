@@ -50,11 +50,13 @@ constexpr int kQT = 32 * kWaves; // queries per workgroup
 constexpr int kKRow = kD + 8;    // K row stride (halves): 272 B, conflict-free b128 fragment reads
 constexpr int kVRow = kKB + 8;   // Vt row stride (halves): 144 B
 
-struct AttnSmem {
-    _Float16 k[2][kKB][kKRow];    // 2 x 17 KiB
-    _Float16 vt[2][kD][kVRow];    // 2 x 18 KiB
+template <int NB>
+struct AttnSmemN {
+    _Float16 k[NB][kKB][kKRow];   // NB x 17 KiB
+    _Float16 vt[NB][kD][kVRow];   // NB x 18 KiB
     float bcast[kWaves][32];      // per-wave per-query factors (alpha, then 1/l)
 };
+using AttnSmem = AttnSmemN<2>;
 
 // Workspace image of one (head, key block): the K tile then the transposed V tile, byte for byte
 // the LDS layout (row padding included), so one 1-KiB LDS-DMA piece per wave-instruction moves it.
@@ -233,20 +235,29 @@ kv_attention_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__ 
     // LDS-DMA of the workspace images: wave w moves pieces w, w + 8, ... (1 KiB each).
     const uint8_t *himg = img + static_cast<size_t>(h) * nkb * kImg + lane * 16;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(wave);
-    auto dma_k = [&](int blk, int buf) {
+    constexpr bool STAG = false;   // v4: no staggered schedule
+    // pieces p0, p0 + step, ... of an image (the whole workgroup: wv, 8; one group: wv % 4, 4)
+    auto dma_k = [&](int blk, int buf, uint32_t p0 = 0xffffffffu, uint32_t step = kWaves) {
         const uint8_t *src = himg + static_cast<size_t>(blk) * kImg;
         const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_addr(&sm.k[buf][0][0]));
-        for (uint32_t p = wv; p < kKImg / 1024; p += kWaves) glds16_asm(src + p * 1024, dst + p * 1024);
+        for (uint32_t p = p0 == 0xffffffffu ? wv : p0; p < kKImg / 1024; p += step) glds16_asm(src + p * 1024, dst + p * 1024);
     };
-    auto dma_v = [&](int blk, int buf) {
+    auto dma_v = [&](int blk, int buf, uint32_t p0 = 0xffffffffu, uint32_t step = kWaves) {
         const uint8_t *src = himg + static_cast<size_t>(blk) * kImg + kKImg;
         const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_addr(&sm.vt[buf][0][0]));
-        for (uint32_t p = wv; p < kVImg / 1024; p += kWaves) glds16_asm(src + p * 1024, dst + p * 1024);
+        for (uint32_t p = p0 == 0xffffffffu ? wv : p0; p < kVImg / 1024; p += step) glds16_asm(src + p * 1024, dst + p * 1024);
     };
-    // Prologue: K and V of block 0 and K of block 1 staged; S^T of block 0 computed.
+    const bool grp_b = STAG && wave >= kWaves / 2;
+    auto raw_barrier = []() __attribute__((always_inline)) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // Prologue: K and V of block 0 and K of block 1 staged (STAG: and V of block 1); S^T of block 0.
     dma_k(0, 0);
     dma_v(0, 0);
     if (nkb > 1) dma_k(1, 1);
+    if (STAG && nkb > 1) dma_v(1, 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     float16_t st[2], sn[2];
@@ -396,12 +407,26 @@ __device__ __forceinline__ float swap_halves_sum(float x) {
 // 16 QK MFMAs back to back and then the whole softmax); the max and sum reductions are trees
 // (depth 5 instead of 32-long chains); the k-loop is unrolled by two so the score register sets
 // swap roles instead of being copied.
-template <int LAB = 0>
+//
+// STAG (A/B, lab case 198): waves 4-7 (group B, the second wave of each SIMD) run half a k-block behind
+// waves 0-3 (group A), so that on every SIMD one wave's region 1 (QK MFMAs + the softmax's exp /
+// max / sum VALU) overlaps the other's region 2 (P V MFMAs, little VALU) instead of both waves
+// reaching the softmax together.  One barrier per half block (group B enters through one extra,
+// group A leaves through one extra); K and V rings of THREE buffers each (K(j), V(j) in buffer
+// j % 3, 105 KiB).  Half-block interval 2 kb: A runs R1(kb), B R2(kb - 1); interval 2 kb + 1: A
+// R2(kb), B R1(kb).  Group A stages K(kb + 2) at the start of its R1(kb) (the buffer's previous
+// block, K(kb - 1), was last read by B in interval 2 kb - 3) and waits for it before the barrier
+// ending interval 2 kb + 1 (first read by A in 2 kb + 2); group B stages V(kb + 2) at the start
+// of its R1(kb) (V(kb - 1) last read by B in 2 kb) and waits for it before the barrier ending
+// interval 2 kb + 2 (first read by A in 2 kb + 5).  Same arithmetic per query as STAG = false:
+// the outputs are bit-identical.
+template <int LAB = 0, bool STAG = false>
 __global__ void __launch_bounds__(kWaves * 64)
 kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__ img, const float *__restrict__ kp,
                     const float *__restrict__ vp, int S, int H, _Float16 *__restrict__ O) {
+    constexpr int NB = STAG ? 3 : 2;
     const int nkb = (S + kKB - 1) / kKB;
-    __shared__ __attribute__((aligned(16))) AttnSmem sm;
+    __shared__ __attribute__((aligned(16))) AttnSmemN<NB> sm;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int h = blockIdx.y;
     const int q0 = blockIdx.x * kQT + wave * 32;
@@ -444,20 +469,28 @@ kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__
     // LDS-DMA of the workspace images: wave w moves pieces w, w + 8, ... (1 KiB each).
     const uint8_t *himg = img + static_cast<size_t>(h) * nkb * kImg + lane * 16;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(wave);
-    auto dma_k = [&](int blk, int buf) {
+    // pieces p0, p0 + step, ... of an image (the whole workgroup: wv, 8; one group: wv % 4, 4)
+    auto dma_k = [&](int blk, int buf, uint32_t p0 = 0xffffffffu, uint32_t step = kWaves) {
         const uint8_t *src = himg + static_cast<size_t>(blk) * kImg;
         const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_addr(&sm.k[buf][0][0]));
-        for (uint32_t p = wv; p < kKImg / 1024; p += kWaves) glds16_asm(src + p * 1024, dst + p * 1024);
+        for (uint32_t p = p0 == 0xffffffffu ? wv : p0; p < kKImg / 1024; p += step) glds16_asm(src + p * 1024, dst + p * 1024);
     };
-    auto dma_v = [&](int blk, int buf) {
+    auto dma_v = [&](int blk, int buf, uint32_t p0 = 0xffffffffu, uint32_t step = kWaves) {
         const uint8_t *src = himg + static_cast<size_t>(blk) * kImg + kKImg;
         const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_addr(&sm.vt[buf][0][0]));
-        for (uint32_t p = wv; p < kVImg / 1024; p += kWaves) glds16_asm(src + p * 1024, dst + p * 1024);
+        for (uint32_t p = p0 == 0xffffffffu ? wv : p0; p < kVImg / 1024; p += step) glds16_asm(src + p * 1024, dst + p * 1024);
     };
-    // Prologue: K and V of block 0 and K of block 1 staged; S^T of block 0 computed.
+    const bool grp_b = STAG && wave >= kWaves / 2;
+    auto raw_barrier = []() __attribute__((always_inline)) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // Prologue: K and V of block 0 and K of block 1 staged (STAG: and V of block 1); S^T of block 0.
     dma_k(0, 0);
     dma_v(0, 0);
     if (nkb > 1) dma_k(1, 1);
+    if (STAG && nkb > 1) dma_v(1, 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     // One k-block: DMAs of the blocks ahead, then region 1 (S^T of block kb+1 on the matrix pipe,
@@ -472,7 +505,12 @@ kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__
         // wave + 8, wave + 16 of each image: a plain 16-B load and a ds_write_b128 per piece).
         // Measured at S 8192 H 32: LDS-DMA 1111 us, register staging 1176 us.
         u32x4_t kr[3], vr[3];
-        if constexpr (!(LAB & 2)) {
+        if constexpr (STAG) {
+            if (more2) {
+                if (!grp_b) dma_k(kb + 2, (kb + 2) % 3, wv, kWaves / 2);
+                else dma_v(kb + 2, (kb + 2) % 3, wv - kWaves / 2, kWaves / 2);
+            }
+        } else if constexpr (!(LAB & 2)) {
             if constexpr (!(LAB & 64)) {
                 if (more2) dma_k(kb + 2, kb & 1);
                 if (more1) dma_v(kb + 1, (kb + 1) & 1);
@@ -505,7 +543,8 @@ kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__
                 }
         }
         // ---- region 1.  After the last block the K buffer is stale: sn is computed and dropped.
-        const auto &kn = sm.k[(kb + 1) & 1];
+        if constexpr (LAB & 512) __builtin_amdgcn_s_setprio(1);   // A/B: priority to region 1
+        const auto &kn = sm.k[(kb + 1) % NB];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
 #pragma unroll
@@ -552,6 +591,8 @@ kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
             __builtin_amdgcn_sched_group_barrier(0x002, 5, 1);
         }
+        if constexpr (LAB & 512) __builtin_amdgcn_s_setprio(0);
+        if constexpr (STAG) raw_barrier();   // the half-block barrier
         // ---- rescale O rows by their query's alpha, only if some query's max moved ----
         if (!(LAB & 1) && !__all(alpha == 1.0f)) {
             if (hh == 0) sm.bcast[wave][ql] = alpha;
@@ -568,7 +609,8 @@ kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__
             }
         }
         // ---- region 2: O += P (q_v - z_v), the P^T accumulator as the A operand ----
-        const auto &vt = sm.vt[kb & 1];
+        if constexpr (LAB & 256) __builtin_amdgcn_s_setprio(1);   // A/B: priority to region 2
+        const auto &vt = sm.vt[kb % NB];
 #pragma unroll
         for (int s2 = 0; s2 < 4; ++s2) {
             const int u = s2 >> 1, sl = s2 & 1;
@@ -603,6 +645,7 @@ kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__
             __builtin_amdgcn_sched_group_barrier(0x002, 5, 2);
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
         }
+        if constexpr (LAB & 256) __builtin_amdgcn_s_setprio(0);
         if constexpr (!(LAB & 2) && (LAB & 64)) {
             asm volatile("s_waitcnt vmcnt(0)"
                          : "+v"(kr[0]), "+v"(kr[1]), "+v"(kr[2]), "+v"(vr[0]), "+v"(vr[1]), "+v"(vr[2])
@@ -616,8 +659,13 @@ kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__
                 *reinterpret_cast<u32x4_t *>(vd + min(static_cast<int>(wv) + 8 * i, kVImg / 1024 - 1) * 1024) = vr[i];
             }
         }
-        if constexpr (!(LAB & 16)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if constexpr (!(LAB & 32)) __syncthreads();
+        if constexpr (STAG) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            raw_barrier();
+        } else {
+            if constexpr (!(LAB & 16)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if constexpr (!(LAB & 32)) __syncthreads();
+        }
     };
     // LAB & 128 (A/B): static priority 1 for the second-dispatched half (waves 4-7), which
     // otherwise loses every VALU arbitration to its older SIMD partner (MI355X_MICROARCH.md, two
@@ -627,10 +675,12 @@ kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__
     }
     float16_t sa[2], sb[2];
     qk(sa, sm.k[0]);
+    if (grp_b) raw_barrier();   // group B enters half a block behind
     for (int kb = 0; kb < nkb; kb += 2) {
         iter(sa, sb, kb);
         if (kb + 1 < nkb) iter(sb, sa, kb + 1);
     }
+    if (STAG && !grp_b) raw_barrier();   // group A joins group B's last barrier
 
     // ---- normalise (1/l and the V scale) and store: o[dt][r] -> query q0 + (r&3) + 8(r>>2) + 4hh ----
     if (hh == 0) sm.bcast[wave][ql] = vs / l_run;
@@ -954,12 +1004,19 @@ extern "C" int dllm_kv_attention(const void *Q, const uint8_t *Kq, const float *
 #define DLLM_ALAB6(L) case 200 + L: kv_attention6_kernel<L><<<grid, kW6 * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh); break;
         DLLM_ALAB6(2) DLLM_ALAB6(4) DLLM_ALAB6(8)
 #undef DLLM_ALAB6
+        case 300: kv_attention5_kernel<256, true><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh); break;
+        case 301: kv_attention5_kernel<512, true><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh); break;
+        case 302: kv_attention5_kernel<256, false><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh); break;
+        case 303: kv_attention5_kernel<512, false><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh); break;
+        case 198:   // the staggered schedule (A/B; bit-identical)
+            kv_attention5_kernel<0, true><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh);
+            break;
         default:
-            kv_attention5_kernel<0><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh);
+            kv_attention5_kernel<0, false><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh);
             break;
     }
 #else
-    kv_attention5_kernel<0><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh);
+    kv_attention5_kernel<0, false><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh);
 #endif
     DLLM_LAUNCH_CHECK();
     return DLLM_OK;

@@ -210,6 +210,51 @@ __device__ __forceinline__ void lds_words(uint32_t (&w)[BITS], const uint8_t *wb
 }
 
 
+// Coalesced f16 store of a block's full output tile through LDS (the drained stage ring `img`,
+// `cap` bytes): rows of 32 NW columns (64 NW bytes), `rows` = 32 MR tokens, written in passes of as
+// many rows as fit.  acc[r] reg 4 qd + j -> token 32 r + (lane & 31), column 32 wave + 4 hsel +
+// 8 qd + j (the 32x32x16 C/D map), each lane's 4 columns one 8-B piece; the 16-B chunk index of a
+// row is XORed with the row (conflict-free 16-lane groups for the 8-B writes and the 16-B reads),
+// and every wave then stores whole rows with 16-B lanes (64 NW / 16 lanes per row) instead of
+// 64 rows x 8 B per instruction.  Ends with the block's waves past a barrier.
+template <int NW, int MR>
+__device__ __forceinline__ void store_tile_f16_lds(uint8_t *img, int cap, const float16_t (&acc)[MR],
+                                                   const float4 (&bv)[4], __half *Y, int N, int m0, int n0,
+                                                   int wave, int lane) {
+    constexpr int kRowB = 64 * NW, kCpr = 4 * NW;                 // row bytes, 16-B chunks per row
+    constexpr int kRows = 32 * MR;
+    const int hsel = lane >> 5;
+    const int per_pass = (cap / kRowB) >= kRows ? kRows : ((cap / kRowB) / 32) * 32;   // whole reps
+    const int c0 = wave * 4;
+    for (int p0 = 0; p0 < kRows; p0 += per_pass) {
+#pragma unroll
+        for (int r = 0; r < MR; ++r) {
+            if (r * 32 < p0 || r * 32 >= p0 + per_pass) continue;
+            const int t = r * 32 - p0 + (lane & 31);
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd) {
+                const int pc = (c0 + qd) ^ (t & (kCpr - 1));
+                union { __half h[4]; uint2 u; } pk;
+                pk.h[0] = __float2half_rn(acc[r][4 * qd + 0] + bv[qd].x);
+                pk.h[1] = __float2half_rn(acc[r][4 * qd + 1] + bv[qd].y);
+                pk.h[2] = __float2half_rn(acc[r][4 * qd + 2] + bv[qd].z);
+                pk.h[3] = __float2half_rn(acc[r][4 * qd + 3] + bv[qd].w);
+                *reinterpret_cast<uint2 *>(img + t * kRowB + pc * 16 + hsel * 8) = pk.u;
+            }
+        }
+        __syncthreads();
+        constexpr int kRowsPerInst = 1024 / kRowB;
+        const int c = lane % kCpr;
+        const int nrows = per_pass < kRows - p0 ? per_pass : kRows - p0;
+        for (int t0 = wave * kRowsPerInst; t0 < nrows; t0 += NW * kRowsPerInst) {
+            const int t = t0 + lane / kCpr;
+            const uint4 v = *reinterpret_cast<const uint4 *>(img + t * kRowB + ((c ^ (t & (kCpr - 1))) * 16));
+            *reinterpret_cast<uint4 *>(Y + static_cast<size_t>(m0 + p0 + t) * N + n0 + 8 * c) = v;
+        }
+        __syncthreads();
+    }
+}
+
 // LDS-DMA issued from inline asm: invisible to hipcc's waitcnt pass, so the only waits on these
 // loads are the counted vmcnt statements placed by hand (guide 5.7, M0 written in the statement).
 template <int BITS, int NW = 8, int MR = kMReps, int KG = 1>
@@ -243,6 +288,7 @@ struct ExactGemmArgs {
     int N, Npad, group;
     const PSampleEpi *epi;
     int tm = 0;   // A/B: 256 x 256 tile-major tiles where they fill the chip
+    int lab_policy = 0;   // lab A/B: 1 = the round-2 tile policy (no 32 x 128 mid-M tiles)
     const float *hr = nullptr;   // Horner ratios (DLLM_EXACT_HORNER builds: the 128 x 256 tiles in Horner form)
 };
 int launch_exact_gemm(const ExactGemmArgs &a, int y_f32, hipStream_t st);

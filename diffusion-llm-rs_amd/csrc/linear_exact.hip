@@ -539,6 +539,12 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
         return;
     }
     const bool full = (m0 + kBMt <= M) && (n0 + kBNt <= N) && (N % 4) == 0;
+    if constexpr (std::is_same<YT, __half>::value && KG == 1 && NW * 64 >= 256) {
+        if (full) {   // coalesced 16-B row stores through the drained ring
+            store_tile_f16_lds<NW, MR>(ring, static_cast<int>(sizeof(ring)), acc, bv, Y, N, m0, n0, wave, lane);
+            return;
+        }
+    }
     if (full) {
 #pragma unroll
         for (int r = 0; r < MR; ++r) {
@@ -630,6 +636,16 @@ int launch_exact_bits(const ExactGemmArgs &a, hipStream_t st) {
         else return launch_exact_tile<BITS, YT, 8, 4, 2, G64 / 2, EPI>(a, 1, st);
     }
     const int tiles = mb * (a.Npad / 128), ngroups = a.K / a.group;
+    // Mid M (int4 g128): 32 x 128 tiles of 4 waves streaming the whole K -- no K split, hence no
+    // f32 slabs and no combine launch -- where they give a full round but 64 x 128 tiles do not
+    // (M 225..448 at N = 4096, where the policy below splits K): M 256 / 384: 25.1 -> 20.4 /
+    // 30.0 -> 24.6 us; at M >= 512 the 64 x 128 two-k-group tiles stay faster (23.1 vs 25.8 us)
+    // (profiles/r03_midm/policy_ab.json).
+    if constexpr (G64 == 2 && BITS == 4 && DLLM_EXACT_WREG) {
+        const int t32 = ((a.M + 31) / 32) * (a.Npad / 128), t64 = ((a.M + 63) / 64) * (a.Npad / 128);
+        if (!a.lab_policy && tiles < kCUs && t64 < kCUs && t32 >= kCUs)
+            return launch_exact_tile<BITS, YT, 4, 1, 2, 1, EPI>(a, 1, st);
+    }
 #if DLLM_EXACT_KG2
     // tile-starved grids: 128 x 128 (or 64 x 128) tiles with two k-groups of 4 waves per block
     if constexpr (G64 == 2 && BITS == 4 && DLLM_EXACT_WREG) {

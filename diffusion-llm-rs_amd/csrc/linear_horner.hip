@@ -71,7 +71,9 @@ __device__ __forceinline__ void horner_burst(__amdgpu_buffer_rsrc_t xr, uint32_t
         : "memory");
 }
 
-// MODE bit 0: the staggered schedule (product); bit 1 (lab ablation only): no output stores.
+// MODE bit 0: the staggered schedule (product).  Lab ablations only (results wrong, timing only):
+// bit 1 no output stores; bit 2 no Horner rescale; bit 3 one dequant per k-step instead of four;
+// bit 4 one B fragment read per k-step instead of four.
 template <typename YT, int EPI, int MODE>
 __global__ void __launch_bounds__(512, 1)
 wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdev,
@@ -147,10 +149,12 @@ wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_setprio(1);
         if (j < 3) {
-            read_b(bn, sb, j + 1);
-            an = dequant_exact<4>(w, j + 1, ec);
+            if constexpr ((MODE & 16) == 0) read_b(bn, sb, j + 1);
+            if constexpr ((MODE & 8) != 0) an = ac;
+            else an = dequant_exact<4>(w, j + 1, ec);
         }
-        if (gf && j == 0) {
+        const half8_t (&bu)[8] = (MODE & 16) ? bA : bc;
+        if ((MODE & 4) == 0 && gf && j == 0) {
             // acc <- acc * r_g right before the group's first MFMA of each rep (scalar v_mul_f32:
             // the file is built without the SLP vectorizer)
 #pragma unroll
@@ -162,7 +166,7 @@ wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
                     acc[r][4 * qd + 2] *= r4[qd].z;
                     acc[r][4 * qd + 3] *= r4[qd].w;
                 }
-                acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bc[r], acc[r], 0, 0, 0);
+                acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bu[r], acc[r], 0, 0, 0);
             }
             // rep i + 1's rescale issues beside rep i's MFMA
             __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
@@ -175,7 +179,7 @@ wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
             }
         } else {
 #pragma unroll
-            for (int r = 0; r < 8; ++r) acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bc[r], acc[r], 0, 0, 0);
+            for (int r = 0; r < 8; ++r) acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bu[r], acc[r], 0, 0, 0);
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -302,40 +306,8 @@ wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
     }
     const bool full = (m0 + 256 <= M) && (n0 + 256 <= N) && (N % 4) == 0;
     if constexpr (std::is_same<YT, __half>::value) {
-        if (full) {
-            // Coalesced f16 store through the (now idle) LDS ring, 128 token rows per pass: each
-            // wave writes its 32 columns of the pass's rows (8-B pieces, 16-B chunk index XORed
-            // with the row: conflict-free per 16-lane group), then every wave stores whole 512-B
-            // rows with 16-B lanes -- 1 KiB per instruction in 2 rows, instead of 64 rows x 8 B.
-            uint8_t *img = smem;
-            const int c0 = wave * 4;   // the wave's first 16-B chunk (8 columns each) of a row
-#pragma unroll
-            for (int pass = 0; pass < 2; ++pass) {
-#pragma unroll
-                for (int rr = 0; rr < 4; ++rr) {
-                    const int r = 4 * pass + rr;
-                    const int t = 32 * rr + (lane & 31);
-#pragma unroll
-                    for (int qd = 0; qd < 4; ++qd) {
-                        const int pc = (c0 + qd) ^ (t & 31);
-                        union { __half h[4]; uint2 u; } pk;
-                        pk.h[0] = __float2half_rn(acc[r][4 * qd + 0] + bv[qd].x);
-                        pk.h[1] = __float2half_rn(acc[r][4 * qd + 1] + bv[qd].y);
-                        pk.h[2] = __float2half_rn(acc[r][4 * qd + 2] + bv[qd].z);
-                        pk.h[3] = __float2half_rn(acc[r][4 * qd + 3] + bv[qd].w);
-                        *reinterpret_cast<uint2 *>(img + t * 512 + pc * 16 + hsel * 8) = pk.u;
-                    }
-                }
-                __syncthreads();
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    const int t = 16 * wave + 2 * i + hsel;
-                    const int c = lane & 31;
-                    const uint4 v = *reinterpret_cast<const uint4 *>(img + t * 512 + ((c ^ (t & 31)) * 16));
-                    *reinterpret_cast<uint4 *>(Y + static_cast<size_t>(m0 + 128 * pass + t) * N + n0 + 8 * c) = v;
-                }
-                if (pass == 0) __syncthreads();
-            }
+        if (full) {   // coalesced 16-B row stores through the drained ring (2 passes of 128 rows)
+            store_tile_f16_lds<8, 8>(smem, 3 * kHStage, acc, bv, Y, N, m0, n0, wave, lane);
             return;
         }
     }
@@ -384,10 +356,14 @@ void launch_horner_t(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
 
 int launch_horner_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
 #if DLLM_LAB
-    if (a.lab == 1 || a.lab == 2 || a.lab == 3) {   // lab A/B: 1 no stagger; 2 / 3: + no stores (ablation)
+    if (a.lab >= 1 && a.lab <= 7) {   // lab A/B: 1 no stagger; 2.. ablations (see MODE)
         if (a.lab == 1) launch_horner_t<0>(a, y_f32, st);
         else if (a.lab == 2) launch_horner_t<3>(a, y_f32, st);
-        else launch_horner_t<2>(a, y_f32, st);
+        else if (a.lab == 3) launch_horner_t<2>(a, y_f32, st);
+        else if (a.lab == 4) launch_horner_t<3 | 4>(a, y_f32, st);
+        else if (a.lab == 5) launch_horner_t<3 | 8>(a, y_f32, st);
+        else if (a.lab == 6) launch_horner_t<3 | 16>(a, y_f32, st);
+        else launch_horner_t<3 | 4 | 8 | 16>(a, y_f32, st);
         DLLM_LAUNCH_CHECK();
         return DLLM_OK;
     }

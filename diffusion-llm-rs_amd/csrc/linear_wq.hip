@@ -1437,10 +1437,12 @@ wq_gemm16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
 typedef float float4_t __attribute__((ext_vector_type(4)));
 constexpr int kDecWaves = 8;
 
-// EXACT: the MFMA A operand is the exact integer (q - zp) (linear_exact.hip) and each slab's
-// partial is folded into the accumulator with the f32 scales of its group(s) (group 64: two folds
-// per 128-deep slab; group >= 128: one).
-template <int BITS, typename YT, int MT, int NT = 1, bool SPLIT = false, int LAB = 0, bool EXACT = false>
+// EXACT (1: group 64, 2: group >= 128): the MFMA A operand is the exact integer (q - zp)
+// (linear_exact.hip) and each slab's partial is folded into the accumulator with the f32 scales of
+// its group(s) (group 64: two folds per 128-deep slab; group >= 128: one).  With one group per
+// slab every lane's own {zp} dword is already its column's for all four 32-deep steps, so EXACT = 2
+// skips the per-step ds_bpermute (an LDS round trip on the dequant's critical path).
+template <int BITS, typename YT, int MT, int NT = 1, bool SPLIT = false, int LAB = 0, int EXACT = 0>
 __global__ void __launch_bounds__(kDecWaves * 64)
 wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdec,
                  const uint32_t *__restrict__ sz, const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad,
@@ -1491,7 +1493,7 @@ wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = float4_t{0.f, 0.f, 0.f, 0.f};
 
-    const bool g64 = group == 64;   // EXACT: two groups per 128-deep slab
+    const bool g64 = EXACT == 1;    // two groups per 128-deep slab
     for (int base = s_beg + wave; base < s_end; base += kDecWaves * kDepth) {
         uint32_t w[kDepth][NT][BITS];
         uint32_t szl[kDepth][NT];
@@ -1547,7 +1549,7 @@ wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
                     float4_t tacc[MT];
 #pragma unroll
                     for (int t = 0; t < 4; ++t) {
-                        const uint32_t szv = static_cast<uint32_t>(
+                        const uint32_t szv = EXACT == 2 ? szl[i][nt] : static_cast<uint32_t>(
                             __builtin_amdgcn_ds_bpermute(((lane & 15) + 16 * t) * 4, static_cast<int>(szl[i][nt])));
                         const half2_t p = __builtin_bit_cast(half2_t, szv);
                         const half8_t a = dequant_exact<BITS>(w[i][nt], t, exact_consts(half2_t{p[0], p[0]}));
@@ -1646,7 +1648,7 @@ inline void decode_policy(int M, int &nt, int &nsplit) {
     nt = nsplit = M > 32 ? 4 : 1;
 }
 
-template <int BITS, typename YT, int MT, int NT, bool EXACT>
+template <int BITS, typename YT, int MT, int NT, int EXACT>
 int launch_decode_nt(const dllm_linear *h, const __half *X, int M, YT *Y, int nsplit, hipStream_t st) {
     const unsigned nbx = static_cast<unsigned>(h->Npad / (16 * NT));
     const int K = static_cast<int>(h->K), N = static_cast<int>(h->N);
@@ -1671,7 +1673,7 @@ int launch_decode_nt(const dllm_linear *h, const __half *X, int M, YT *Y, int ns
     return DLLM_OK;
 }
 
-template <int BITS, typename YT, int MT, bool EXACT>
+template <int BITS, typename YT, int MT, int EXACT>
 int launch_decode_mt(const dllm_linear *h, const __half *X, int M, YT *Y, int nt, int nsplit, hipStream_t st) {
     switch (nt) {
     case 2: return launch_decode_nt<BITS, YT, MT, 2, EXACT>(h, X, M, Y, nsplit, st);
@@ -1680,7 +1682,7 @@ int launch_decode_mt(const dllm_linear *h, const __half *X, int M, YT *Y, int nt
     }
 }
 
-template <int BITS, typename YT, bool EXACT>
+template <int BITS, typename YT, int EXACT>
 int launch_decode_x(const dllm_linear *h, const __half *X, size_t M, YT *Y, int nt, int nsplit, hipStream_t st) {
     const int Mi = static_cast<int>(M);
     if (M <= 16) return launch_decode_mt<BITS, YT, 1, EXACT>(h, X, Mi, Y, nt, nsplit, st);
@@ -1725,8 +1727,11 @@ int launch_decode(const dllm_linear *h, const __half *X, size_t M, YT *Y, hipStr
 #endif
     // the column group must tile Npad (a multiple of 128)
     while (nt > 1 && h->Npad % (16 * nt)) nt /= 2;
-    if (use_exact(h)) return launch_decode_x<BITS, YT, true>(h, X, M, Y, nt, nsplit, st);
-    return launch_decode_x<BITS, YT, false>(h, X, M, Y, nt, nsplit, st);
+    if (use_exact(h)) {
+        if (h->group == 64) return launch_decode_x<BITS, YT, 1>(h, X, M, Y, nt, nsplit, st);
+        return launch_decode_x<BITS, YT, 2>(h, X, M, Y, nt, nsplit, st);
+    }
+    return launch_decode_x<BITS, YT, 0>(h, X, M, Y, nt, nsplit, st);
 }
 
 // 3-stage-ring GEMM (rounded weights) with tile (32 MR) x (32 NW), K optionally split into nsplit slices.
@@ -1937,6 +1942,7 @@ int launch_horner(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream
     HornerGemmArgs a{X, M, (int)h->K, h->wdev, h->sz, h->hr, h->sf, h->bias, Y, (int)h->N, (int)h->Npad, epi};
 #if DLLM_LAB
     if (h->variant >= 25 && h->variant <= 27) a.lab = h->variant - 24;   // lab A/B (see HornerGemmArgs::lab)
+    if (h->variant >= 29 && h->variant <= 31) a.lab = h->variant - 25;   // lab ablations 4..6
 #endif
     return launch_horner_gemm(a, std::is_same<YT, float>::value ? 1 : 0, st);
 }
@@ -1946,6 +1952,7 @@ inline ExactGemmArgs exact_args(const dllm_linear *h, const __half *X, int M, vo
                     (int)h->group, epi};
 #if DLLM_LAB
     a.tm = h->variant == 15 ? 1 : 0;
+    a.lab_policy = h->variant == 28 ? 1 : 0;
 #endif
     return a;
 }
@@ -2348,8 +2355,8 @@ int dllm_linear_set_kernel_variant(dllm_linear_t h, int variant) {
         h->pplab = (variant - 100) % 32;
         return DLLM_OK;
     }
-    if (variant < -1 || (variant > 15 && (variant < 24 || variant > 27)))
-        return fail(DLLM_ERR_INVALID_PARAMS, "variant must be -1..15 or 24..27 (16..23, 32..95, 100..195, 200..263: ablations)");
+    if (variant < -1 || (variant > 15 && (variant < 24 || variant > 31)))
+        return fail(DLLM_ERR_INVALID_PARAMS, "variant must be -1..15 or 24..31 (16..23, 32..95, 100..195, 200..263: ablations)");
     h->variant = variant;
     h->dlab = h->rlab = h->pplab = h->dcfg = 0;
     return DLLM_OK;
