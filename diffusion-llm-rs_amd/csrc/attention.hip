@@ -543,7 +543,6 @@ kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__
                 }
         }
         // ---- region 1.  After the last block the K buffer is stale: sn is computed and dropped.
-        if constexpr (LAB & 512) __builtin_amdgcn_s_setprio(1);   // A/B: priority to region 1
         const auto &kn = sm.k[(kb + 1) % NB];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
@@ -591,7 +590,6 @@ kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
             __builtin_amdgcn_sched_group_barrier(0x002, 5, 1);
         }
-        if constexpr (LAB & 512) __builtin_amdgcn_s_setprio(0);
         if constexpr (STAG) raw_barrier();   // the half-block barrier
         // ---- rescale O rows by their query's alpha, only if some query's max moved ----
         if (!(LAB & 1) && !__all(alpha == 1.0f)) {
@@ -609,7 +607,9 @@ kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__
             }
         }
         // ---- region 2: O += P (q_v - z_v), the P^T accumulator as the A operand ----
-        if constexpr (LAB & 256) __builtin_amdgcn_s_setprio(1);   // A/B: priority to region 2
+        // Static priority 1 over region 2 (P V MFMAs): a SIMD whose other wave is in its softmax VALU
+        // keeps issuing MFMAs (measured at S 8192, H 32: 1.0447 vs 1.0645 ms; LAB & 256 drops it, A/B).
+        if constexpr (!(LAB & 256)) __builtin_amdgcn_s_setprio(1);
         const auto &vt = sm.vt[kb % NB];
 #pragma unroll
         for (int s2 = 0; s2 < 4; ++s2) {
@@ -645,7 +645,7 @@ kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__
             __builtin_amdgcn_sched_group_barrier(0x002, 5, 2);
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
         }
-        if constexpr (LAB & 256) __builtin_amdgcn_s_setprio(0);
+        if constexpr (!(LAB & 256)) __builtin_amdgcn_s_setprio(0);
         if constexpr (!(LAB & 2) && (LAB & 64)) {
             asm volatile("s_waitcnt vmcnt(0)"
                          : "+v"(kr[0]), "+v"(kr[1]), "+v"(kr[2]), "+v"(vr[0]), "+v"(vr[1]), "+v"(vr[2])
@@ -1004,10 +1004,9 @@ extern "C" int dllm_kv_attention(const void *Q, const uint8_t *Kq, const float *
 #define DLLM_ALAB6(L) case 200 + L: kv_attention6_kernel<L><<<grid, kW6 * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh); break;
         DLLM_ALAB6(2) DLLM_ALAB6(4) DLLM_ALAB6(8)
 #undef DLLM_ALAB6
-        case 300: kv_attention5_kernel<256, true><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh); break;
-        case 301: kv_attention5_kernel<512, true><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh); break;
-        case 302: kv_attention5_kernel<256, false><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh); break;
-        case 303: kv_attention5_kernel<512, false><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh); break;
+        case 302:   // the product without the region-2 priority (A/B; bit-identical)
+            kv_attention5_kernel<256, false><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh);
+            break;
         case 198:   // the staggered schedule (A/B; bit-identical)
             kv_attention5_kernel<0, true><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh);
             break;

@@ -307,6 +307,9 @@ struct HornerGemmArgs {
     int lab = 0;   // lab build only: 1 = the unstaggered schedule (A/B); 2 / 3 = staggered / not, no stores
 };
 int launch_horner_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st);
+// The same Horner form on 256 x 128 tiles with two k-groups per tile (linear_horner.hip): needs
+// K % 256 == 0 and Npad % 128 == 0.
+int launch_horner_kg2_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st);
 bool exact_gemm_supported(int M, int K, int Npad, int group);
 
 // Ping-pong 256 x 256 GEMM (linear_pp.hip): Y = X . W^ + b for the 256-column-tile grid, bits in

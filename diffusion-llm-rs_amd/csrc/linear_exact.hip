@@ -103,12 +103,12 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
     static_assert(!HORN || (KPG == 1 && !TM && KG == 1 && !SPLIT && (GPS == 1 || RING == 2)), "Horner form: whole-group stages, whole K");
     static_assert(!WREG || (BITS == 4 && !TM), "register-staged weight words: int4, group-major stages");
     static_assert(GPS == 1 || (KPG == 1 && !TM && (4 * SPS) % GPS == 0 && 2 * GPS <= NW), "whole groups per stage");
-    static_assert(RING == 3 || (RING == 2 && !TM), "ring depth");
+    static_assert(RING == 3 || (RING >= 2 && RING <= 8 && !TM), "ring depth");
     static_assert(KG == 1 || (!TM && RING * KG * SL::kBytes >= NW * 64 * MR * 16 * 4), "k-group combine fits the ring");
     constexpr int kBMt = 32 * MR, kBNt = 32 * NW;
     // RING stages of KG parts each (k-group g's part of stage i at ring + (i KG + g) kBytes)
     __shared__ __attribute__((aligned(16))) uint8_t ring[RING * KG * SL::kBytes];
-    uint8_t *const st0 = ring, *const st1 = ring + KG * SL::kBytes, *const st2 = ring + 2 * KG * SL::kBytes;
+    auto stp = [&](int i) __attribute__((always_inline)) { return ring + i * KG * SL::kBytes; };   // ring slot i
 
     // XCD-aware order: consecutive work items land on one XCD (blocks b, b+8 share an XCD under
     // round-robin dispatch); K-slice outermost so an XCD's blocks share the slice's X rows in L2.
@@ -193,10 +193,12 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
         if (has_sf) blds16_asm(prs, poff, goff, u(base + SL::kX + SL::kW + SL::kSZ + pg * 1024));
     };
     // Counted wait leaving the newest stage's DMAs (this wave's own count) in flight.
+    // (RING > 3: the RING - 2 newest stages stay in flight.)
+    static_assert((RING - 2) * (SL::kXRounds + SL::kWOps + 1) <= 63, "vmcnt range");
     auto wait_prev = [&]() __attribute__((always_inline)) {
         if constexpr (RING == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else if (has_sz || has_sf) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kXRounds + SL::kWOps + 1) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kXRounds + SL::kWOps) : "memory");
+        else if (has_sz || has_sf) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((RING - 2) * (SL::kXRounds + SL::kWOps + 1)) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((RING - 2) * (SL::kXRounds + SL::kWOps)) : "memory");
     };
 
     float16_t acc[MR], tacc[TM ? TMB : MR];
@@ -446,18 +448,23 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
     auto at = [&](auto i_tag, unsigned kt) __attribute__((always_inline)) {
         constexpr int I = decltype(i_tag)::value;
         constexpr int cur = I % RING, nxt = (I + RING - 1) % RING;
-        uint8_t *sb = (cur == 0 ? st0 : (cur == 1 ? st1 : st2)) + kpart;
-        uint8_t *pf = (nxt == 0 ? st0 : (nxt == 1 ? st1 : st2)) + kpart;
+        uint8_t *sb = stp(cur) + kpart;
+        uint8_t *pf = stp(nxt) + kpart;
         if constexpr (TM) step_tm(sb, pf, kt);
         else step(sb, pf, kt, std::integral_constant<bool, I % KPG == 0>{},
                   std::integral_constant<bool, I % KPG == KPG - 1>{}, std::integral_constant<int, cur>{});
     };
-    constexpr int kUnroll = RING == 2 ? (KPG == 1 ? 2 : 4) : ((KPG == 1 || TM) ? 3 : (KPG == 2 ? 6 : 12));
+    constexpr int kUnroll = RING == 2 ? (KPG == 1 ? 2 : 4)
+                          : RING == 3 ? ((KPG == 1 || TM) ? 3 : (KPG == 2 ? 6 : 12))
+                                      : (KPG == 1 ? RING : (RING % KPG == 0 ? RING : RING * KPG));
 
-    stage(st0 + kpart, 0, std::integral_constant<int, 0>{});
-    if constexpr (RING == 3) {
-        if (nk > 1) stage(st1 + kpart, 1, std::integral_constant<int, 1>{});
-        if (nk > 1) wait_prev();
+    stage(stp(0) + kpart, 0, std::integral_constant<int, 0>{});
+    if constexpr (RING >= 3) {
+        // stages 1 .. RING - 2 in flight before the loop (stage kt + RING - 1 is issued in step kt)
+        [&]<int... Is>(std::integer_sequence<int, Is...>) __attribute__((always_inline)) {
+            ((Is + 1 < static_cast<int>(nk) ? (stage(stp(Is + 1) + kpart, Is + 1, std::integral_constant<int, Is + 1>{}), 0) : 0), ...);
+        }(std::make_integer_sequence<int, RING - 2>{});
+        if (nk >= RING - 1) wait_prev();
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -611,6 +618,11 @@ int launch_exact_tile(const ExactGemmArgs &a, int nsplit, hipStream_t st) {
 // 3. (MR2) 64 x 128 tiles (4 waves) while 128 x 128 tiles give < 512 blocks, K split until >= 512;
 // 4. 128 x 128 tiles (4 waves, two blocks per CU, 64-deep stages) with K split over group-aligned
 //    slices until the grid has >= ~200 blocks.
+// Mid-M 32 x 128 tiles: LDS stages in the ring (10 KiB each; the weight words ride in VGPRs).  A
+// block streams 512 KiB of X and weight words at K = 4096 with one wave per SIMD, so its rate is
+// the bytes it keeps in flight: RING - 1 stages.
+constexpr int kMidRing = 6;
+
 template <int BITS, typename YT, int G64, int EPI>
 int launch_exact_bits(const ExactGemmArgs &a, hipStream_t st) {
     const int mb = (a.M + 127) / 128;
@@ -643,8 +655,17 @@ int launch_exact_bits(const ExactGemmArgs &a, hipStream_t st) {
     // (profiles/r03_midm/policy_ab.json).
     if constexpr (G64 == 2 && BITS == 4 && DLLM_EXACT_WREG) {
         const int t32 = ((a.M + 31) / 32) * (a.Npad / 128), t64 = ((a.M + 63) / 64) * (a.Npad / 128);
-        if (!a.lab_policy && tiles < kCUs && t64 < kCUs && t32 >= kCUs)
-            return launch_exact_tile<BITS, YT, 4, 1, 2, 1, EPI>(a, 1, st);
+        if (a.lab_policy != 1 && tiles < kCUs && t64 < kCUs && t32 >= kCUs) {
+#if DLLM_LAB
+            switch (a.lab_policy) {   // lab A/B of the ring depth
+            case 2: return launch_exact_tile<BITS, YT, 4, 1, 2, 1, EPI, false, 1, 3>(a, 1, st);
+            case 3: return launch_exact_tile<BITS, YT, 4, 1, 2, 1, EPI, false, 1, 4>(a, 1, st);
+            case 4: return launch_exact_tile<BITS, YT, 4, 1, 2, 1, EPI, false, 1, 8>(a, 1, st);
+            default: break;
+            }
+#endif
+            return launch_exact_tile<BITS, YT, 4, 1, 2, 1, EPI, false, 1, kMidRing>(a, 1, st);
+        }
     }
 #if DLLM_EXACT_KG2
     // tile-starved grids: 128 x 128 (or 64 x 128) tiles with two k-groups of 4 waves per block

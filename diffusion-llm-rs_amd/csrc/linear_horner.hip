@@ -335,6 +335,329 @@ wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// KG2 Horner GEMM: 256-token x 128-column tiles for grids where 256 x 256 tiles leave CUs idle
+// (M = 2048 at N = 4096, 11 of the 12 GEMMs of a C5 step: 128 tiles of 256 x 256, 256 of
+// 256 x 128; a 2-GPU column shard at M = 4096 likewise).  8 waves = 4 column waves (32 columns x
+// 256 tokens each, wq_horner_kernel's wave tile, acc = 8 x 16 f32) x 2 k-groups: k-group kg runs the
+// Horner chain over the groups of K-half kg (the ratio at a half's first group multiplies a zero
+// accumulator), so each SIMD holds one wave of each k-group and every wave does the same work per
+// k-step as in wq_horner_kernel.  A stage holds k-step kt of both halves: the two X slices
+// (2 x 32 KiB), the 8 waves' weight words (8 KiB) and, on a group's first k-step, both halves'
+// {zp, scale} pairs and ratios (4 x 512 B, each loaded twice by a 64-lane DMA); 2 stages in a ring
+// (152 KiB), stage kt + 1 issued while kt computes, one vmcnt(0) + barrier per k-step.
+// Epilogue: Y = acc0 s_{G/2-1} + acc1 s_{G-1} + b.  K-group 1 hands its scaled accumulator to its
+// column partner through the drained ring, k-group 0 adds it (P0 + P1, a fixed order), and all 8
+// waves store the f16 tile as coalesced 16-B rows.
+constexpr int kKX = 256 * kBK * 2;              // one K-half's X slice per stage (32 KiB)
+constexpr int kKW = 8 * 1024;                   // 8 waves x 1 KiB of weight words
+constexpr int kKG = 4 * 1024;                   // 2 halves x (sz, ratios) x 1 KiB (mirrored halves)
+constexpr int kKStage = 2 * kKX + kKW + kKG;    // 77824 B; 2 stages = 152 KiB
+
+// One wave's stage burst: 8 X pieces (its k-group's slice, pieces 4 i + nw: rows (4 i + nw) 8 ..,
+// 4 KiB apart in LDS) and its weight words.
+__device__ __forceinline__ void kg2_burst(__amdgpu_buffer_rsrc_t xr, const uint32_t (&xo)[8], uint32_t sx,
+                                          __amdgpu_buffer_rsrc_t wr, uint32_t wo, uint32_t sw, uint32_t lds_x,
+                                          uint32_t lds_w) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %13\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %9, %10 offen lds\n\t"
+        "s_add_u32 m0, m0, 0x1000\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %2, %9, %10 offen lds\n\t"
+        "s_add_u32 m0, m0, 0x1000\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %3, %9, %10 offen lds\n\t"
+        "s_add_u32 m0, m0, 0x1000\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %4, %9, %10 offen lds\n\t"
+        "s_add_u32 m0, m0, 0x1000\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %5, %9, %10 offen lds\n\t"
+        "s_add_u32 m0, m0, 0x1000\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %6, %9, %10 offen lds\n\t"
+        "s_add_u32 m0, m0, 0x1000\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %7, %9, %10 offen lds\n\t"
+        "s_add_u32 m0, m0, 0x1000\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %8, %9, %10 offen lds\n\t"
+        "s_mov_b32 m0, %14\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %11, %12, %15 offen lds\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(xo[0]), "v"(xo[1]), "v"(xo[2]), "v"(xo[3]), "v"(xo[4]), "v"(xo[5]), "v"(xo[6]), "v"(xo[7]),
+          "s"(xr), "s"(sx), "v"(wo), "s"(wr), "s"(lds_x), "s"(lds_w), "s"(sw)
+        : "memory");
+}
+
+template <typename YT, int EPI>
+__global__ void __launch_bounds__(512, 1)
+wq_horner_kg2_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdev,
+                     const uint32_t *__restrict__ sz, const float *__restrict__ hr, const float *__restrict__ sf,
+                     const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad, int nbm, int nbn,
+                     PSampleEpi epi) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kKStage];
+
+    // XCD-aware bijective remap (as wq_horner_kernel): an XCD's 32 concurrent tiles are one
+    // 256-row block x 32 column blocks at N = 4096, so its L2 holds one X row block.
+    const int nb = nbm * nbn, orig = blockIdx.x;
+    const int xcd = orig % kXCDs, q8 = nb / kXCDs, r8 = nb % kXCDs;
+    const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / kXCDs;
+    const int bm = tile / nbn, bn = tile % nbn;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int kg = wave >> 2, nw = wave & 3;
+    const int m0 = bm * 256, n0 = bn * 128;
+    const int nk = K / kBK, nk2 = nk / 2;   // k-steps per K-half (even: K % 256 == 0)
+    const int kofs = kg * nk2;              // this k-group's first k-step
+
+    uint32_t xo[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int row = (i * 4 + nw) * 8 + (lane >> 3);
+        const int rrow = (m0 + row < M ? m0 + row : M - 1) - m0;   // rows past M re-read row M - 1
+        const int c = (lane & 7) ^ ((row >> 1) & 7);
+        xo[i] = static_cast<uint32_t>((rrow * K + c * 8) * 2);
+    }
+    const __amdgpu_buffer_rsrc_t xr = raw_rsrc(X + static_cast<size_t>(m0) * K);
+    const uint32_t nt = static_cast<uint32_t>(n0 + 32 * nw) >> 5;
+    const __amdgpu_buffer_rsrc_t wr = raw_rsrc(wdev + static_cast<size_t>(nt) * nk * 64 * 4);
+    const uint32_t wo = static_cast<uint32_t>(lane * 16);
+    // group data: column wave 0 of each k-group stages the {zp, scale} pairs of columns n0 .. n0+127,
+    // column wave 1 the ratios; lanes 32..63 repeat lanes 0..31 (a full 64-lane DMA, no exec mask)
+    const __amdgpu_buffer_rsrc_t gr =
+        raw_rsrc(nw == 0 ? static_cast<const void *>(sz + n0) : static_cast<const void *>(hr + n0));
+    const bool has_g = nw < 2;
+    const uint32_t go = static_cast<uint32_t>((lane & 31) * 16);
+    const uint32_t sbase = __builtin_amdgcn_readfirstlane(lds_addr(smem));
+
+    auto stage = [&](int slot, int kt, bool gf) __attribute__((always_inline)) {
+        const uint32_t base = sbase + static_cast<uint32_t>(slot * kKStage);
+        const int ka = kofs + kt;
+        kg2_burst(xr, xo, static_cast<uint32_t>(ka * kBK * 2), wr, wo, static_cast<uint32_t>(ka * 1024),
+                  base + static_cast<uint32_t>(kg * kKX + nw * 1024), base + static_cast<uint32_t>(2 * kKX + wave * 1024));
+        if (gf && has_g)
+            blds16_asm(gr, go, static_cast<uint32_t>((ka >> 1) * Npad * 4),
+                       base + static_cast<uint32_t>(2 * kKX + kKW + kg * 2048 + nw * 1024));
+    };
+
+    float16_t acc[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[r][e] = 0.0f;
+
+    const int hsel = lane >> 5;
+    const int rowx = ((lane & 31) >> 1) & 7;
+    int soff[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) soff[s] = (lane & 31) * (kBK * 2) + ((((2 * s + hsel) ^ rowx)) << 4);
+
+    auto read_b = [&](half8_t (&b)[8], const uint8_t *sb, int s) __attribute__((always_inline)) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) b[r] = *reinterpret_cast<const half8_t *>(sb + soff[s] + r * 32 * kBK * 2);
+    };
+
+    ExactConsts ec;
+    uint32_t w[4];
+    float4 r4[4];
+    half8_t bA[8], bB[8], aA, aB;
+    auto sub = [&](const uint8_t *sb, half8_t (&bc)[8], half8_t (&bn)[8], const half8_t &ac, half8_t &an, int j,
+                   bool gf) __attribute__((always_inline)) {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+        if (j < 3) {
+            read_b(bn, sb, j + 1);
+            an = dequant_exact<4>(w, j + 1, ec);
+        }
+        if (gf && j == 0) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+#pragma unroll
+                for (int qd = 0; qd < 4; ++qd) {
+                    acc[r][4 * qd + 0] *= r4[qd].x;
+                    acc[r][4 * qd + 1] *= r4[qd].y;
+                    acc[r][4 * qd + 2] *= r4[qd].z;
+                    acc[r][4 * qd + 3] *= r4[qd].w;
+                }
+                acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bc[r], acc[r], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                if (i + 1 < 8) __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bc[r], acc[r], 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+            }
+        }
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto barrier = []() __attribute__((always_inline)) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // One k-step of this k-group's half on ring slot `slot`; slot ^ 1 receives k-step kt + 1
+    // (the slot's previous k-step, kt - 1, was read before the barrier that ended it).
+    auto step = [&](int slot, int kt, auto gf_tag) __attribute__((always_inline)) {
+        constexpr bool GF = decltype(gf_tag)::value;
+        if (kt + 1 < nk2) stage(slot ^ 1, kt + 1, !GF);   // kt + 1 opens a group iff kt does not
+        const uint8_t *st8 = smem + slot * kKStage;
+        const uint8_t *sb = st8 + kg * kKX;
+        {
+            const uint4 v = *reinterpret_cast<const uint4 *>(st8 + 2 * kKX + wave * 1024 + lane * 16);
+            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+        }
+        if constexpr (GF) {
+            const uint8_t *gb = st8 + 2 * kKX + kKW + kg * 2048;
+            half2_t nz, sc;
+            split_sz(*reinterpret_cast<const uint32_t *>(gb + (nw * 32 + (lane & 31)) * 4), nz, sc);
+            ec = exact_consts(nz);
+            const float *rl = reinterpret_cast<const float *>(gb + 1024) + nw * 32 + 4 * hsel;
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd) r4[qd] = *reinterpret_cast<const float4 *>(rl + 8 * qd);
+        }
+        read_b(bA, sb, 0);
+        aA = dequant_exact<4>(w, 0, ec);
+        sub(sb, bA, bB, aA, aB, 0, GF);
+        sub(sb, bB, bA, aB, aA, 1, GF);
+        sub(sb, bA, bB, aA, aB, 2, GF);
+        sub(sb, bB, bA, aB, aA, 3, GF);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // k-step kt + 1 landed
+        barrier();
+    };
+
+    stage(0, 0, true);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    using GFt = std::integral_constant<bool, true>;
+    using GFf = std::integral_constant<bool, false>;
+    for (int kt = 0; kt < nk2; kt += 2) {   // group = 2 k-steps = the 2-slot ring period
+        step(0, kt, GFt{});
+        step(1, kt + 1, GFf{});
+    }
+
+    // this half's partial sum: acc times the half's last group scales
+    const int nb0 = n0 + nw * 32 + 4 * hsel;
+    const float *sl = sf + static_cast<size_t>((kofs + nk2) / 2 - 1) * Npad + nb0;
+#pragma unroll
+    for (int qd = 0; qd < 4; ++qd) {
+        const float4 s = *reinterpret_cast<const float4 *>(sl + 8 * qd);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            acc[r][4 * qd + 0] *= s.x;
+            acc[r][4 * qd + 1] *= s.y;
+            acc[r][4 * qd + 2] *= s.z;
+            acc[r][4 * qd + 3] *= s.w;
+        }
+    }
+    // k-group 1 -> LDS (the ring is drained: every DMA waited for, every wave past the last
+    // barrier); 4 column waves x 8 reps x 4 x 1 KiB = 128 KiB, one 16-B piece per lane
+    float4 *part = reinterpret_cast<float4 *>(smem);
+    if (kg == 1) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd)
+                part[((nw * 8 + r) * 4 + qd) * 64 + lane] =
+                    make_float4(acc[r][4 * qd + 0], acc[r][4 * qd + 1], acc[r][4 * qd + 2], acc[r][4 * qd + 3]);
+    }
+    __syncthreads();
+    if (kg == 0) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd) {
+                const float4 v = part[((nw * 8 + r) * 4 + qd) * 64 + lane];
+                acc[r][4 * qd + 0] = acc[r][4 * qd + 0] + v.x;
+                acc[r][4 * qd + 1] = acc[r][4 * qd + 1] + v.y;
+                acc[r][4 * qd + 2] = acc[r][4 * qd + 2] + v.z;
+                acc[r][4 * qd + 3] = acc[r][4 * qd + 3] + v.w;
+            }
+    }
+    __syncthreads();
+    float4 bv[4];
+#pragma unroll
+    for (int qd = 0; qd < 4; ++qd) bv[qd] = *reinterpret_cast<const float4 *>(bias + nb0 + 8 * qd);
+    if constexpr (EPI == 1) {
+        if (kg != 0) return;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const int m = m0 + r * 32 + (lane & 31);
+            if (m >= M) continue;
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd) {
+                if (nb0 + 8 * qd >= N) continue;
+                psample4(epi, m, nb0 + 8 * qd, N, acc[r][4 * qd + 0] + bv[qd].x, acc[r][4 * qd + 1] + bv[qd].y,
+                         acc[r][4 * qd + 2] + bv[qd].z, acc[r][4 * qd + 3] + bv[qd].w);
+            }
+        }
+        return;
+    }
+    const bool full = (m0 + 256 <= M) && (n0 + 128 <= N) && (N % 8) == 0;
+    if constexpr (std::is_same<YT, __half>::value) {
+        if (full) {
+            // k-group 0 writes the f16 tile image (256 rows x 256 B, 16-B chunks XORed with the
+            // row), then all 8 waves store 4 whole rows per instruction
+            uint8_t *img = smem;
+            if (kg == 0) {
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    const int t = r * 32 + (lane & 31);
+#pragma unroll
+                    for (int qd = 0; qd < 4; ++qd) {
+                        const int pc = (nw * 4 + qd) ^ (t & 15);
+                        union { __half h[4]; uint2 u; } pk;
+                        pk.h[0] = __float2half_rn(acc[r][4 * qd + 0] + bv[qd].x);
+                        pk.h[1] = __float2half_rn(acc[r][4 * qd + 1] + bv[qd].y);
+                        pk.h[2] = __float2half_rn(acc[r][4 * qd + 2] + bv[qd].z);
+                        pk.h[3] = __float2half_rn(acc[r][4 * qd + 3] + bv[qd].w);
+                        *reinterpret_cast<uint2 *>(img + t * 256 + pc * 16 + hsel * 8) = pk.u;
+                    }
+                }
+            }
+            __syncthreads();
+            const int c = lane & 15;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int t = (i * 8 + wave) * 4 + (lane >> 4);
+                const uint4 v = *reinterpret_cast<const uint4 *>(img + t * 256 + ((c ^ (t & 15)) * 16));
+                *reinterpret_cast<uint4 *>(Y + static_cast<size_t>(m0 + t) * N + n0 + 8 * c) = v;
+            }
+            return;
+        }
+    }
+    if (kg != 0) return;
+    const bool vec_ok = (N % 4) == 0;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const int m = m0 + r * 32 + (lane & 31);
+        if (m >= M) continue;
+        YT *yrow = Y + static_cast<size_t>(m) * N;
+#pragma unroll
+        for (int qd = 0; qd < 4; ++qd)
+            store_out4<YT>(yrow, bias, nb0 + 8 * qd, N, vec_ok, acc[r][4 * qd + 0], acc[r][4 * qd + 1],
+                           acc[r][4 * qd + 2], acc[r][4 * qd + 3]);
+    }
+}
 
 template <int MODE>
 void launch_horner_t(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
@@ -353,6 +676,23 @@ void launch_horner_t(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
 }
 
 }  // namespace
+
+int launch_horner_kg2_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
+    const int nbm = (a.M + 255) / 256, nbn = a.Npad / 128;
+    const unsigned nb = static_cast<unsigned>(nbm * nbn);
+    const PSampleEpi ep = a.epi ? *a.epi : PSampleEpi{};
+    if (a.epi)
+        wq_horner_kg2_kernel<float, 1><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
+                                                          a.epi->x_prev, a.N, a.Npad, nbm, nbn, ep);
+    else if (y_f32)
+        wq_horner_kg2_kernel<float, 0><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
+                                                          static_cast<float *>(a.Y), a.N, a.Npad, nbm, nbn, ep);
+    else
+        wq_horner_kg2_kernel<__half, 0><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
+                                                           static_cast<__half *>(a.Y), a.N, a.Npad, nbm, nbn, ep);
+    DLLM_LAUNCH_CHECK();
+    return DLLM_OK;
+}
 
 int launch_horner_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
 #if DLLM_LAB

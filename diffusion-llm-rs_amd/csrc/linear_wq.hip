@@ -1918,6 +1918,24 @@ bool horner_ready(const dllm_linear *hc, int M, hipStream_t st) {
     return ensure_horner(hc, st);
 }
 
+// The KG2 Horner kernel (256 x 128 tiles, two k-groups): where neither the 256 x 256 Horner grid
+// nor the fold form's 128 x 256 grid fills a round but the 256 x 128 grid does (N = 4096: M
+// 1793..1920; measured at M = 1800: 69.2 vs 74.9 us).  At M = 2048 the 128 x 256 fold grid fills
+// the chip and is as fast (68.5 vs 69.6 us: KG2 stages two K-halves' X slices, 72 KiB per k-step
+// against 24 KiB for the same MFMAs; profiles/r03_kg2/).
+bool horner_kg2_ready(const dllm_linear *hc, int M) {
+    const int np = static_cast<int>(hc->Npad);
+    if (!(hc->precision == DLLM_PRECISION_EXACT && hc->bits == 4 && hc->group == 128 && hc->K % 256 == 0 &&
+          np % 128 == 0 && hc->hstate == 1))
+        return false;
+#if DLLM_LAB
+    if (hc->variant == 14 || hc->variant == 28) return false;   // lab A/B: the fold-form exact policy
+#endif
+    const int t256 = ((M + 255) / 256) * (np / 256), tk = ((M + 255) / 256) * (np / 128);
+    const int t128 = ((M + 127) / 128) * (np / 256);
+    return t256 < kCUs && t128 < kCUs && tk >= kCUs;
+}
+
 template <typename YT, int EPI>
 int launch_horner(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t st, const PSampleEpi *epi) {
 #if DLLM_LAB
@@ -1952,7 +1970,7 @@ inline ExactGemmArgs exact_args(const dllm_linear *h, const __half *X, int M, vo
                     (int)h->group, epi};
 #if DLLM_LAB
     a.tm = h->variant == 15 ? 1 : 0;
-    a.lab_policy = h->variant == 28 ? 1 : 0;
+    a.lab_policy = h->variant == 28 ? 1 : (h->variant >= 300 && h->variant <= 302 ? h->variant - 298 : 0);
 #endif
     return a;
 }
@@ -1974,6 +1992,11 @@ int launch_prefill_auto(const dllm_linear *h, const __half *X, int M, YT *Y, hip
 #endif
     if (use_exact(h)) {
         if (BITS == 4 && horner_ready(h, M, st)) return launch_horner<YT, EPI>(h, X, M, Y, st, epi);
+        if (BITS == 4 && horner_kg2_ready(h, M)) {
+            const HornerGemmArgs a{X, M, (int)h->K, h->wdev, h->sz, h->hr, h->sf, h->bias, Y, (int)h->N,
+                                   (int)h->Npad, epi};
+            return launch_horner_kg2_gemm(a, std::is_same<YT, float>::value ? 1 : 0, st);
+        }
         ExactGemmArgs a = exact_args(h, X, M, Y, epi);
 #if DLLM_EXACT_HORNER   // A/B build: the 128 x 256 exact tiles in Horner form too
         if (BITS == 4 && ensure_horner(h, st)) a.hr = h->hr;
@@ -2355,8 +2378,8 @@ int dllm_linear_set_kernel_variant(dllm_linear_t h, int variant) {
         h->pplab = (variant - 100) % 32;
         return DLLM_OK;
     }
-    if (variant < -1 || (variant > 15 && (variant < 24 || variant > 31)))
-        return fail(DLLM_ERR_INVALID_PARAMS, "variant must be -1..15 or 24..31 (16..23, 32..95, 100..195, 200..263: ablations)");
+    if (variant < -1 || (variant > 15 && (variant < 24 || variant > 31) && (variant < 300 || variant > 302)))
+        return fail(DLLM_ERR_INVALID_PARAMS, "variant must be -1..15, 24..31 or 300..302 (16..23, 32..95, 100..195, 200..263: ablations)");
     h->variant = variant;
     h->dlab = h->rlab = h->pplab = h->dcfg = 0;
     return DLLM_OK;

@@ -1,8 +1,7 @@
 """A/B of the dequant-attention schedules on config C4 (S 8192, 32 heads x 128, int4 KV), lab build,
 one process (DLLM_ATTN_LAB is read per call), interleaved rounds, HIP events: 0 = the product
-(v5), 198 = v5 with waves 4-7 staggered by half a key block, 300 / 301 = staggered with s_setprio 1
-around region 2 / region 1, 302 / 303 = the same priorities unstaggered.  The outputs must be
-bit-identical.
+(v5 with s_setprio 1 over region 2), 302 = v5 without that priority, 198 = v5 with waves 4-7
+staggered by half a key block.  The outputs must be bit-identical.
 Also checks ragged S (partial key blocks / query tiles).  Measurement only."""
 import json
 import os
@@ -15,7 +14,7 @@ import torch
 import __graft_entry__ as g
 
 d = g.load_package(); d.load_library()
-labs = [int(v) for v in (sys.argv[1:] or ["0", "198", "300", "301", "302", "303"])]
+labs = [int(v) for v in (sys.argv[1:] or ["0", "302", "198"])]
 
 
 def run(lab, Q, e):

@@ -427,12 +427,13 @@ def test_linear_split_k_exact_integers(dllm, torch, orc):
 
 @pytest.mark.parametrize("precision", [0, 1])
 @pytest.mark.parametrize("bits", [2, 4, 8])
-@pytest.mark.parametrize("M,N", [(4096, 4096), (2048, 4096), (4096, 1024), (4096, 512), (512, 1024), (300, 256),
-                                 (64, 200), (33, 200), (17, 200), (1, 200)])
+@pytest.mark.parametrize("M,N", [(4096, 4096), (2048, 4096), (1800, 4096), (4096, 1024), (4096, 512), (512, 1024),
+                                 (300, 256), (64, 200), (33, 200), (17, 200), (1, 200)])
 def test_linear_policy_exact_integers(dllm, torch, orc, precision, bits, M, N):
     """Every tile of both precision policies on exact-integer data (each group spans [0, 2^b - 1]:
     scale 1, zp 0; K = 768 = 6 groups, so every product and partial sum is an exact integer):
-    exact weights -- 128 x 256 tiles (M 4096 / 2048 at N 4096), 128 x 128 + group-aligned split-K
+    exact weights -- 128 x 256 tiles (M 4096 / 2048 at N 4096), the KG2 Horner tiles (int4, M 1800),
+    128 x 128 + group-aligned split-K
     (N 1024 / 512, M 512, 300), the exact decode kernel (M <= 64, one or 4 column tiles, K split) --
     and rounded weights (256 x 256, 256 x 128 two k-groups, 128 x 128 split-K, decode), with bias,
     ragged M and a padded last column group: bit-equal to the f64 product, f32 and f16 outputs."""
@@ -477,10 +478,14 @@ def test_linear_exact_weights_tight(dllm, torch, orc, M, N, group):
     lin.close()
 
 
-@pytest.mark.parametrize("spread,M,K", [(8, 4096, 4096), (8, 8000, 1024), (8, 4300, 1024), (30, 4096, 2048), (45, 4096, 1024)])
+@pytest.mark.parametrize("spread,M,K", [(8, 4096, 4096), (8, 8000, 1024), (8, 4300, 1024), (30, 4096, 2048), (45, 4096, 1024),
+                                         (8, 1800, 4096), (30, 1850, 2048), (45, 1800, 1024)])
 def test_linear_horner_scale_spread(dllm, torch, orc, spread, M, K):
     """The 256 x 256-tile exact kernel (int4 g128, >= 256 tiles) keeps one accumulator in Horner form:
-    acc <- acc * (s_{g-1} / s_g) + T_g, times s_{G-1} at the end.  Per-(group, column) weight
+    acc <- acc * (s_{g-1} / s_g) + T_g, times s_{G-1} at the end; at M = 1800 / 1850 (120 such tiles,
+    240 of the fold form's 128 x 256) the 256 x 128-tile KG2 kernel runs one chain per K-half (the
+    second starting from a zero accumulator) and sums the two halves' partials times their last
+    scales.  Per-(group, column) weight
     magnitudes spread by 2^U(-spread, spread): every column is checked on its own against f32 on the
     same f16 X with the reference's a2 weights (quantization.rs:81-85), so a group rescaled wrongly
     shows even where other groups dominate the column.  spread 45 gives columns whose scales span
@@ -581,12 +586,14 @@ def test_linear_decode_first_call_in_capture(dllm, torch):
     ref.close()
 
 
-def test_linear_horner_first_call_in_capture(dllm, torch, orc):
-    """The forward contract: a handle's first call on a Horner grid (M = K = N = 4096, int4 g128)
-    made inside stream capture runs the same kernel as every later eager call -- the Horner ratios
-    were decided at create, nothing is allocated or synchronised by the call -- so the graph replay
-    and two eager calls are bit-identical, within the exact-weights bound of f32 on the same f16 X."""
-    K = N = M = 4096
+@pytest.mark.parametrize("M", [4096, 1800])
+def test_linear_horner_first_call_in_capture(dllm, torch, orc, M):
+    """The forward contract: a handle's first call on a Horner grid (K = N = 4096, int4 g128; M 4096:
+    256 x 256 tiles, M 1800: the KG2 256 x 128 tiles) made inside stream capture runs the same
+    kernel as every later eager call -- the Horner ratios were decided at create, nothing is
+    allocated or synchronised by the call -- so the graph replay and two eager calls are
+    bit-identical, within the exact-weights bound of f32 on the same f16 X."""
+    K = N = 4096
     g = torch.Generator(device="cuda").manual_seed(4242)
     W = 0.02 * torch.randn(K, N, device="cuda", generator=g)
     X = torch.randn(M, K, device="cuda", generator=g).half()
