@@ -92,7 +92,7 @@ struct ExactStage {
 // k-group 0's first: a tile-starved grid gets two waves per SIMD without a second launch.
 template <int BITS, typename YT, int NW, int MR, int SPS, int KPG, bool SPLIT = false, int EPI = 0, bool TM = false,
           int TMB = 1, bool WREG = false, int GPS = 1, int RING = 3, int KG = 1, bool HORN = false>
-__global__ void __launch_bounds__(NW * KG * 64, NW * KG == 8 ? 1 : 2)
+__global__ void __launch_bounds__(NW * KG * 64, NW * KG >= 8 ? 1 : 2)
 wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdev,
                      const uint32_t *__restrict__ sz, const float *__restrict__ sf, const float *__restrict__ bias,
                      YT *__restrict__ Y, int N, int Npad, int group, int nbm, int nbn, int nsplit = 1,
@@ -104,7 +104,7 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
     static_assert(!WREG || (BITS == 4 && !TM), "register-staged weight words: int4, group-major stages");
     static_assert(GPS == 1 || (KPG == 1 && !TM && (4 * SPS) % GPS == 0 && 2 * GPS <= NW), "whole groups per stage");
     static_assert(RING == 3 || (RING >= 2 && RING <= 8 && !TM), "ring depth");
-    static_assert(KG == 1 || (!TM && RING * KG * SL::kBytes >= NW * 64 * MR * 16 * 4), "k-group combine fits the ring");
+    static_assert(KG == 1 || (!TM && RING * KG * SL::kBytes >= (KG - 1) * NW * 64 * MR * 16 * 4), "k-group combine fits the ring");
     constexpr int kBMt = 32 * MR, kBNt = 32 * NW;
     // RING stages of KG parts each (k-group g's part of stage i at ring + (i KG + g) kBytes)
     __shared__ __attribute__((aligned(16))) uint8_t ring[RING * KG * SL::kBytes];
@@ -492,25 +492,30 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
             }
         }
     }
-    if constexpr (KG == 2) {
-        // k-group 1 hands its sums to k-group 0 through the (drained) ring: 16 B per lane per store.
+    if constexpr (KG >= 2) {
+        // k-groups 1 .. KG-1 hand their sums to k-group 0 through the (drained) ring, 16 B per lane
+        // per store; k-group 0 adds them in k-group order.
+        constexpr int kXg = NW * MR * 4 * 64;   // float4s per k-group
         float4 *xch = reinterpret_cast<float4 *>(ring) + (wave * MR * 4) * 64 + lane;
-        if (kg == 1) {
+        if (kg >= 1) {
 #pragma unroll
             for (int r = 0; r < MR; ++r)
 #pragma unroll
                 for (int qd = 0; qd < 4; ++qd)
-                    xch[(r * 4 + qd) * 64] = make_float4(acc[r][4 * qd], acc[r][4 * qd + 1], acc[r][4 * qd + 2], acc[r][4 * qd + 3]);
+                    xch[(kg - 1) * kXg + (r * 4 + qd) * 64] =
+                        make_float4(acc[r][4 * qd], acc[r][4 * qd + 1], acc[r][4 * qd + 2], acc[r][4 * qd + 3]);
         }
         __syncthreads();
-        if (kg == 1) return;
+        if (kg >= 1) return;
 #pragma unroll
-        for (int r = 0; r < MR; ++r)
+        for (int g = 1; g < KG; ++g)
 #pragma unroll
-            for (int qd = 0; qd < 4; ++qd) {
-                const float4 o = xch[(r * 4 + qd) * 64];
-                acc[r][4 * qd] += o.x; acc[r][4 * qd + 1] += o.y; acc[r][4 * qd + 2] += o.z; acc[r][4 * qd + 3] += o.w;
-            }
+            for (int r = 0; r < MR; ++r)
+#pragma unroll
+                for (int qd = 0; qd < 4; ++qd) {
+                    const float4 o = xch[(g - 1) * kXg + (r * 4 + qd) * 64];
+                    acc[r][4 * qd] += o.x; acc[r][4 * qd + 1] += o.y; acc[r][4 * qd + 2] += o.z; acc[r][4 * qd + 3] += o.w;
+                }
     }
     // Epilogue: acc[r] reg e -> n = n0 + 32 wave + 4 hsel + 8 (e >> 2) + (e & 3), m = m0 + 32 r + (lane & 31).
     const int nb0 = n0 + wave * 32 + 4 * hsel;
@@ -618,10 +623,12 @@ int launch_exact_tile(const ExactGemmArgs &a, int nsplit, hipStream_t st) {
 // 3. (MR2) 64 x 128 tiles (4 waves) while 128 x 128 tiles give < 512 blocks, K split until >= 512;
 // 4. 128 x 128 tiles (4 waves, two blocks per CU, 64-deep stages) with K split over group-aligned
 //    slices until the grid has >= ~200 blocks.
-// Mid-M 32 x 128 tiles: LDS stages in the ring (10 KiB each; the weight words ride in VGPRs).  A
-// block streams 512 KiB of X and weight words at K = 4096 with one wave per SIMD, so its rate is
-// the bytes it keeps in flight: RING - 1 stages.
-constexpr int kMidRing = 6;
+// Mid-M 32 x 128 tiles: LDS stages in the ring (10 KiB each; the weight words ride in VGPRs).
+// Deeper rings keep more of a block's 512 KiB (X + weight words at K = 4096) in flight but measured
+// no gain (M 256 / 384: RING 3 / 4 / 6 / 8 = 20.6 / 20.6 / 20.4 / 20.8 and 24.6 / 24.0 / 24.5 / 26.3
+// us, profiles/r03_midm/ring_depth.jsonl): the single wave per SIMD is issue/latency bound, not
+// fed short of bytes.
+constexpr int kMidRing = 3;
 
 template <int BITS, typename YT, int G64, int EPI>
 int launch_exact_bits(const ExactGemmArgs &a, hipStream_t st) {
@@ -657,13 +664,17 @@ int launch_exact_bits(const ExactGemmArgs &a, hipStream_t st) {
         const int t32 = ((a.M + 31) / 32) * (a.Npad / 128), t64 = ((a.M + 63) / 64) * (a.Npad / 128);
         if (a.lab_policy != 1 && tiles < kCUs && t64 < kCUs && t32 >= kCUs) {
 #if DLLM_LAB
-            switch (a.lab_policy) {   // lab A/B of the ring depth
-            case 2: return launch_exact_tile<BITS, YT, 4, 1, 2, 1, EPI, false, 1, 3>(a, 1, st);
-            case 3: return launch_exact_tile<BITS, YT, 4, 1, 2, 1, EPI, false, 1, 4>(a, 1, st);
-            case 4: return launch_exact_tile<BITS, YT, 4, 1, 2, 1, EPI, false, 1, 8>(a, 1, st);
+            switch (a.lab_policy) {   // lab A/B: one k-group (RING 3) / four k-groups (RING 2, 3)
+            case 2: return launch_exact_tile<BITS, YT, 4, 1, 2, 1, EPI, false, 1, kMidRing>(a, 1, st);
+            case 3: if (ngroups % 4 == 0) return launch_exact_tile<BITS, YT, 4, 1, 2, 1, EPI, false, 1, 2, 4>(a, 1, st);
+                    break;
+            case 4: if (ngroups % 4 == 0) return launch_exact_tile<BITS, YT, 4, 1, 2, 1, EPI, false, 1, 3, 4>(a, 1, st);
+                    break;
             default: break;
             }
 #endif
+            // two k-groups of 4 waves (two waves per SIMD): M 256 / 384: 20.4 -> 15.7 / 24.5 -> 23.6 us
+            if (ngroups % 2 == 0) return launch_exact_tile<BITS, YT, 4, 1, 2, 1, EPI, false, 1, 2, 2>(a, 1, st);
             return launch_exact_tile<BITS, YT, 4, 1, 2, 1, EPI, false, 1, kMidRing>(a, 1, st);
         }
     }

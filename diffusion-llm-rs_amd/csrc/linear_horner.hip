@@ -73,7 +73,8 @@ __device__ __forceinline__ void horner_burst(__amdgpu_buffer_rsrc_t xr, uint32_t
 
 // MODE bit 0: the staggered schedule (product).  Lab ablations only (results wrong, timing only):
 // bit 1 no output stores; bit 2 no Horner rescale; bit 3 one dequant per k-step instead of four;
-// bit 4 one B fragment read per k-step instead of four.
+// bit 4 one B fragment read per k-step instead of four; bit 5 no X DMA (weight words only); bit 6
+// no DMA at all.
 template <typename YT, int EPI, int MODE>
 __global__ void __launch_bounds__(512, 1)
 wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdev,
@@ -116,9 +117,15 @@ wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
 
     auto stage = [&](int slot, int kt, bool gf) __attribute__((always_inline)) {
         const uint32_t base = sbase + static_cast<uint32_t>(slot * kHStage);
-        horner_burst(xr, xo[0], xo[1], xo[2], xo[3], static_cast<uint32_t>(kt * kBK * 2), wr, wo,
-                     static_cast<uint32_t>(kt * 1024), base + static_cast<uint32_t>(wave * 1024));
-        if (gf && has_g)
+        if constexpr ((MODE & 64) != 0) {
+            // lab ablation: no DMA at all
+        } else if constexpr ((MODE & 32) != 0) {   // lab ablation: the weight words only
+            blds16_asm(wr, wo, static_cast<uint32_t>(kt * 1024), base + static_cast<uint32_t>(kHX + wave * 1024));
+        } else {
+            horner_burst(xr, xo[0], xo[1], xo[2], xo[3], static_cast<uint32_t>(kt * kBK * 2), wr, wo,
+                         static_cast<uint32_t>(kt * 1024), base + static_cast<uint32_t>(wave * 1024));
+        }
+        if ((MODE & 64) == 0 && gf && has_g)
             blds16_asm(gr, wo, static_cast<uint32_t>((kt >> 1) * Npad * 4),
                        base + static_cast<uint32_t>(kHX + kHW + wave * 1024));
     };
@@ -696,14 +703,16 @@ int launch_horner_kg2_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
 
 int launch_horner_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
 #if DLLM_LAB
-    if (a.lab >= 1 && a.lab <= 7) {   // lab A/B: 1 no stagger; 2.. ablations (see MODE)
+    if (a.lab >= 1 && a.lab <= 9) {   // lab A/B: 1 no stagger; 2.. ablations (see MODE)
         if (a.lab == 1) launch_horner_t<0>(a, y_f32, st);
         else if (a.lab == 2) launch_horner_t<3>(a, y_f32, st);
         else if (a.lab == 3) launch_horner_t<2>(a, y_f32, st);
         else if (a.lab == 4) launch_horner_t<3 | 4>(a, y_f32, st);
         else if (a.lab == 5) launch_horner_t<3 | 8>(a, y_f32, st);
         else if (a.lab == 6) launch_horner_t<3 | 16>(a, y_f32, st);
-        else launch_horner_t<3 | 4 | 8 | 16>(a, y_f32, st);
+        else if (a.lab == 7) launch_horner_t<3 | 4 | 8 | 16>(a, y_f32, st);
+        else if (a.lab == 8) launch_horner_t<3 | 32>(a, y_f32, st);
+        else launch_horner_t<3 | 64>(a, y_f32, st);
         DLLM_LAUNCH_CHECK();
         return DLLM_OK;
     }
