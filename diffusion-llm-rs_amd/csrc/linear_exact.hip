@@ -664,16 +664,22 @@ int launch_exact_bits(const ExactGemmArgs &a, hipStream_t st) {
         const int t32 = ((a.M + 31) / 32) * (a.Npad / 128), t64 = ((a.M + 63) / 64) * (a.Npad / 128);
         if (a.lab_policy != 1 && tiles < kCUs && t64 < kCUs && t32 >= kCUs) {
 #if DLLM_LAB
-            switch (a.lab_policy) {   // lab A/B: one k-group (RING 3) / four k-groups (RING 2, 3)
+            switch (a.lab_policy) {   // lab A/B: one k-group (RING 3) / two k-groups / four (RING 3)
             case 2: return launch_exact_tile<BITS, YT, 4, 1, 2, 1, EPI, false, 1, kMidRing>(a, 1, st);
-            case 3: if (ngroups % 4 == 0) return launch_exact_tile<BITS, YT, 4, 1, 2, 1, EPI, false, 1, 2, 4>(a, 1, st);
+            case 3: if (ngroups % 2 == 0) return launch_exact_tile<BITS, YT, 4, 1, 2, 1, EPI, false, 1, 2, 2>(a, 1, st);
                     break;
             case 4: if (ngroups % 4 == 0) return launch_exact_tile<BITS, YT, 4, 1, 2, 1, EPI, false, 1, 3, 4>(a, 1, st);
                     break;
             default: break;
             }
 #endif
-            // two k-groups of 4 waves (two waves per SIMD): M 256 / 384: 20.4 -> 15.7 / 24.5 -> 23.6 us
+            // k-groups of 4 waves sharing the tile (k-group g streams the g-th part of K; sums handed
+            // to k-group 0 through the ring): four (16 waves, one block per CU) while the grid is
+            // one block per CU, else two (8 waves, two blocks per CU fit).  M 256: 20.4 (one
+            // k-group) -> 15.5 (two) -> 14.3 us (four); M 384: 24.5 -> 22.1 (two) / 25.1 (four)
+            // (profiles/r03_midm/kgroups.jsonl).
+            if (t32 <= kCUs && ngroups % 4 == 0)
+                return launch_exact_tile<BITS, YT, 4, 1, 2, 1, EPI, false, 1, 2, 4>(a, 1, st);
             if (ngroups % 2 == 0) return launch_exact_tile<BITS, YT, 4, 1, 2, 1, EPI, false, 1, 2, 2>(a, 1, st);
             return launch_exact_tile<BITS, YT, 4, 1, 2, 1, EPI, false, 1, kMidRing>(a, 1, st);
         }

@@ -1442,8 +1442,8 @@ constexpr int kDecWaves = 8;
 // its group(s) (group 64: two folds per 128-deep slab; group >= 128: one).  With one group per
 // slab every lane's own {zp} dword is already its column's for all four 32-deep steps, so EXACT = 2
 // skips the per-step ds_bpermute (an LDS round trip on the dequant's critical path).
-template <int BITS, typename YT, int MT, int NT = 1, bool SPLIT = false, int LAB = 0, int EXACT = 0>
-__global__ void __launch_bounds__(kDecWaves * 64)
+template <int BITS, typename YT, int MT, int NT = 1, bool SPLIT = false, int LAB = 0, int EXACT = 0, int DW = kDecWaves>
+__global__ void __launch_bounds__(DW * 64)
 wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdec,
                  const uint32_t *__restrict__ sz, const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad,
                  int group, int nsplit = 1, float *__restrict__ ws = nullptr, const float *__restrict__ sf = nullptr) {
@@ -1456,9 +1456,10 @@ wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
     // returns zeros without a memory access; X is thereby also free of per-lane selects.
     // Rounds of slabs in flight per wave, sized to the registers one slab's operands take.
     constexpr int kPerSlab = NT * BITS + NT + 16 * MT + (EXACT ? 8 * NT : 0);
-    constexpr int kDepth = NT == 1 ? (MT <= 2 ? 4 : 2) : (128 / kPerSlab < 1 ? 1 : (128 / kPerSlab > 4 ? 4 : 128 / kPerSlab));
+    constexpr int kDepth0 = NT == 1 ? (MT <= 2 ? 4 : 2) : (128 / kPerSlab < 1 ? 1 : (128 / kPerSlab > 4 ? 4 : 128 / kPerSlab));
+    constexpr int kDepth = DW > 8 && kDepth0 > 2 ? 2 : kDepth0;   // 16 waves: 2 slabs each at K = 4096
     constexpr uint32_t kOOB = 0x80000000u;
-    __shared__ __attribute__((aligned(16))) float red[kDecWaves * MT * NT * 64 * 4];
+    __shared__ __attribute__((aligned(16))) float red[DW * MT * NT * 64 * 4];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int n0 = blockIdx.x * 16 * NT;
@@ -1494,14 +1495,14 @@ wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
         for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = float4_t{0.f, 0.f, 0.f, 0.f};
 
     const bool g64 = EXACT == 1;    // two groups per 128-deep slab
-    for (int base = s_beg + wave; base < s_end; base += kDecWaves * kDepth) {
+    for (int base = s_beg + wave; base < s_end; base += DW * kDepth) {
         uint32_t w[kDepth][NT][BITS];
         uint32_t szl[kDepth][NT];
         half8_t xb[kDepth][4][MT];
         float4 sfl[kDepth][NT][EXACT ? 2 : 1];
 #pragma unroll
         for (int i = 0; i < kDepth; ++i) {
-            const int slab_raw = base + i * kDecWaves;
+            const int slab_raw = base + i * DW;
             const int slab = min(slab_raw, s_end - 1);
             const int ks = min(slab * 128 + sz_step * 32, K - 32);
 #pragma unroll
@@ -1598,10 +1599,10 @@ wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
             *reinterpret_cast<float4_t *>(red + ((wave * MT * NT + nt * MT + mt) * 64 + lane) * 4) = acc[nt][mt];
     __syncthreads();
     // Wave j sums the 8 partials of tiles j, j + 8, ... (tile = nt * MT + mt) in wave order.
-    for (int tile = wave; tile < MT * NT; tile += kDecWaves) {
+    for (int tile = wave; tile < MT * NT; tile += DW) {
         float4_t s = float4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int w = 0; w < kDecWaves; ++w)
+        for (int w = 0; w < DW; ++w)
             s += *reinterpret_cast<const float4_t *>(red + ((w * MT * NT + tile) * 64 + lane) * 4);
         const int nt = tile / MT, mt = tile % MT;
         const int m = mt * 16 + (lane & 15);
@@ -1656,6 +1657,16 @@ int launch_decode_nt(const dllm_linear *h, const __half *X, int M, YT *Y, int ns
     const int nslab = (K + 127) / 128;
     nsplit = std::max(1, std::min(nsplit, nslab));
     if (nsplit == 1) {
+#if DLLM_LAB
+        if constexpr (MT * NT <= 2) {
+            if (h->variant == 306) {   // lab A/B: 16 waves per block (two slabs each at K = 4096)
+                wq_decode_kernel<BITS, YT, MT, NT, false, 0, EXACT, 16><<<nbx, 16 * 64, 0, st>>>(
+                    X, M, K, h->wdec, h->sz, h->bias, Y, N, Np, gr, 1, nullptr, h->sf);
+                DLLM_LAUNCH_CHECK();
+                return DLLM_OK;
+            }
+        }
+#endif
         wq_decode_kernel<BITS, YT, MT, NT, false, 0, EXACT><<<nbx, kDecWaves * 64, 0, st>>>(
             X, M, K, h->wdec, h->sz, h->bias, Y, N, Np, gr, 1, nullptr, h->sf);
         DLLM_LAUNCH_CHECK();
@@ -2379,8 +2390,8 @@ int dllm_linear_set_kernel_variant(dllm_linear_t h, int variant) {
         h->pplab = (variant - 100) % 32;
         return DLLM_OK;
     }
-    if (variant < -1 || (variant > 15 && (variant < 24 || variant > 31) && (variant < 300 || variant > 304)))
-        return fail(DLLM_ERR_INVALID_PARAMS, "variant must be -1..15, 24..31 or 300..304 (16..23, 32..95, 100..195, 200..263: ablations)");
+    if (variant < -1 || (variant > 15 && (variant < 24 || variant > 31) && (variant < 300 || variant > 306)))
+        return fail(DLLM_ERR_INVALID_PARAMS, "variant must be -1..15, 24..31 or 300..306 (16..23, 32..95, 100..195, 200..263: ablations)");
     h->variant = variant;
     h->dlab = h->rlab = h->pplab = h->dcfg = 0;
     return DLLM_OK;

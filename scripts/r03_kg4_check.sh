@@ -15,4 +15,5 @@ step pt 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -p no:cach
     -k "linear_policy or mid_m or split_k or int4_shapes or exact_weights or first_call" &&
 step kg1 200 python -u scripts/policy_ab.py 300 256 320 384 448 &&
 step kg4r2 200 python -u scripts/policy_ab.py 301 256 384 &&
-step kg4r3 200 python -u scripts/policy_ab.py 302 256 384
+step kg4r3 200 python -u scripts/policy_ab.py 302 256 384 &&
+step dec16 300 python -u scripts/decode_ab.py 306 1 16 32

@@ -383,8 +383,9 @@ def test_linear_full_size_vs_torch_fp32(dllm, torch, orc):
 
 @pytest.mark.parametrize("M", [65, 256, 512, 1024, 1500, 2048])
 def test_linear_mid_m_paths_vs_torch_fp32(dllm, torch, orc, M):
-    """Mid-M dispatch at K=N=4096: 128-row tiles with K split into 8/4/2 slices (M = 65/256/512,
-    slab partials + ordered combine) or unsplit (1024, 1500), and the 256-row tile (2048), each
+    """Mid-M dispatch at K=N=4096: 128-row tiles with K split into 8 slices (M = 65, slab partials +
+    ordered combine), 32 x 128 tiles with four k-groups (256), 64 x 128 tiles with two k-groups
+    (512), 128-row tiles (1024, 1500), and the 128 x 256 tile (2048), each
     within tolerance of the f32 product of the exported weights, for f16 and f32 outputs with
     bias; the other schedules (variants 3, 5, 6) agree too."""
     K = N = 4096
@@ -408,6 +409,25 @@ def test_linear_mid_m_paths_vs_torch_fp32(dllm, torch, orc, M):
     rel = (torch.linalg.norm(Yv - Yr) / torch.linalg.norm(Yr)).item()
     assert rel <= REL_TOL, (M, "f16 weights", rel)
     lin16.close()
+    lin.close()
+
+
+@pytest.mark.parametrize("M,K,N", [(256, 4096, 4096), (384, 4096, 4096), (240, 1024, 4096), (300, 768, 4096)])
+def test_linear_mid_m_kgroups_exact_integers(dllm, torch, orc, M, K, N):
+    """The mid-M 32 x 128 tiles on exact-integer data: four k-groups (M 256 / 240: one block per CU),
+    two (M 384 / 300; K = 768 has 6 groups), k-groups 1.. handing their sums to k-group 0 through
+    the ring.  Every partial sum is an exact integer below 2^24, so the result equals the f64
+    product bit for bit."""
+    rng = np.random.default_rng(M + K)
+    W = rng.integers(0, 16, (K, N)).astype(np.float32)
+    for g0 in range(0, K, 128):
+        W[g0, :], W[g0 + 1, :] = 0.0, 15.0
+    X = rng.integers(-2, 3, (M, K)).astype(np.float32)
+    lin = dllm.QuantLinear.from_weight(dev(torch, W), None, 4, 128)
+    Y = host(lin(dev(torch, X).half(), out_dtype=torch.float32))
+    assert np.array_equal(Y, (X.astype(np.float64) @ W.astype(np.float64)).astype(np.float32))
+    Yh = host(lin(dev(torch, X).half(), out_dtype=torch.float16).float())
+    assert np.array_equal(Yh, Y.astype(np.float16).astype(np.float32))
     lin.close()
 
 
