@@ -104,7 +104,6 @@ SIGNATURES = {
     "dllm_linear_create": (INT, [P, P, S, S, U8, S, P, P]),
     "dllm_linear_create_quantized": (INT, [P, P, P, P, S, S, U8, S, P, P]),
     "dllm_linear_forward": (INT, [P, P, S, INT, P, INT, P]),
-    "dllm_linear_forward_prefetch": (INT, [P, P, S, INT, P, INT, P, P]),
     "dllm_linear_export": (INT, [P, P, P, P, P]),
     "dllm_linear_info": (INT, [P, P, P, P, P]),
     "dllm_linear_weight_bytes": (S, [P]),

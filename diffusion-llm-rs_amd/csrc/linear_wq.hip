@@ -1442,20 +1442,11 @@ constexpr int kDecWaves = 8;
 // its group(s) (group 64: two folds per 128-deep slab; group >= 128: one).  With one group per
 // slab every lane's own {zp} dword is already its column's for all four 32-deep steps, so EXACT = 2
 // skips the per-step ds_bpermute (an LDS round trip on the dequant's critical path).
-//
-// PF (dllm_linear_forward_prefetch): the block also loads one dword of every 128-B line of the next
-// layer's decode words and scales that the same block of the next layer's launch (same shape, hence
-// the same grid) reads, right behind its own first round of loads: under the round-robin dispatch
-// that block runs on the same XCD, so a chain of layers starts each layer on L2-resident weights.
-// The values are only consumed (by an empty asm) at the end, so nothing waits on them earlier.
-template <int BITS, typename YT, int MT, int NT = 1, bool SPLIT = false, int LAB = 0, int EXACT = 0, int DW = kDecWaves,
-          bool PF = false>
+template <int BITS, typename YT, int MT, int NT = 1, bool SPLIT = false, int LAB = 0, int EXACT = 0, int DW = kDecWaves>
 __global__ void __launch_bounds__(DW * 64)
 wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdec,
                  const uint32_t *__restrict__ sz, const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad,
-                 int group, int nsplit = 1, float *__restrict__ ws = nullptr, const float *__restrict__ sf = nullptr,
-                 const uint32_t *__restrict__ pw = nullptr, const uint32_t *__restrict__ psz = nullptr,
-                 const float *__restrict__ psf = nullptr) {
+                 int group, int nsplit = 1, float *__restrict__ ws = nullptr, const float *__restrict__ sf = nullptr) {
     // Slabs in flight per wave: every load of a round (W words, scales, X fragments) is issued
     // before the first MFMA, so a round costs one memory latency, not one per 32-deep step.
     // The load phase has no branch and every loop bound is wave-uniform (scalar wave index): a
@@ -1504,7 +1495,6 @@ wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
         for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = float4_t{0.f, 0.f, 0.f, 0.f};
 
     const bool g64 = EXACT == 1;    // two groups per 128-deep slab
-    uint32_t pfv[2][3] = {{0u, 0u, 0u}, {0u, 0u, 0u}};
     for (int base = s_beg + wave; base < s_end; base += DW * kDepth) {
         uint32_t w[kDepth][NT][BITS];
         uint32_t szl[kDepth][NT];
@@ -1546,34 +1536,6 @@ wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
                         xb[i][t][mt] = __builtin_bit_cast(
                             half8_t, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
                     }
-                }
-            }
-        }
-        if constexpr (PF) {
-            if (base == s_beg + wave) {   // first round (wave-uniform): the next layer's lines
-                // weight words: NT runs (one per n16 tile) of the slice's slabs, 2 BITS lines per slab;
-                // then the scale rows of the slice's groups ({zp, scale} pairs and f32 scales share
-                // the [G][Npad] indexing), 16 NT columns = 64 NT bytes per row
-                constexpr int kGL = NT == 4 ? 2 : 1;
-                const int lpt = (s_end - s_beg) * 2 * BITS, lw = NT * lpt;
-                const int g_lo = s_beg * 128 / group, g_hi = (min(s_end * 128, K) - 1) / group;
-                const int lg = (g_hi - g_lo + 1) * kGL;
-                const __amdgpu_buffer_rsrc_t rw = raw_rsrc(pw + static_cast<size_t>(blockIdx.x) * NT * nslab * 64 * BITS);
-                const __amdgpu_buffer_rsrc_t rs = raw_rsrc(psz + n0), rf = raw_rsrc(psf + n0);
-#pragma unroll
-                for (int p = 0; p < 2; ++p) {
-                    const int l = tid + p * DW * 64;
-                    uint32_t ow = kOOB, og = kOOB;
-                    if (l < lw) {
-                        const int t = l / lpt, j = l - t * lpt;
-                        ow = static_cast<uint32_t>((t * nslab + s_beg) * 64 * BITS * 4 + j * 128);
-                    } else if (l - lw < lg) {
-                        const int r = (l - lw) / kGL, c = (l - lw) - r * kGL;
-                        og = static_cast<uint32_t>((g_lo + r) * Npad * 4 + c * 128);
-                    }
-                    pfv[p][0] = __builtin_amdgcn_raw_buffer_load_b32(rw, ow, 0, 0);
-                    pfv[p][1] = __builtin_amdgcn_raw_buffer_load_b32(rs, og, 0, 0);
-                    pfv[p][2] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_raw_buffer_load_b32(rf, og, 0, 0));
                 }
             }
         }
@@ -1667,9 +1629,6 @@ wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
             }
         }
     }
-    if constexpr (PF)
-        asm volatile("" ::"v"(pfv[0][0]), "v"(pfv[0][1]), "v"(pfv[0][2]), "v"(pfv[1][0]), "v"(pfv[1][1]),
-                     "v"(pfv[1][2]));
 }
 
 constexpr int kDecodeMaxM = 64;
@@ -1691,8 +1650,7 @@ inline void decode_policy(int M, int &nt, int &nsplit) {
 }
 
 template <int BITS, typename YT, int MT, int NT, int EXACT>
-int launch_decode_nt(const dllm_linear *h, const __half *X, int M, YT *Y, int nsplit, hipStream_t st,
-                     const dllm_linear *next) {
+int launch_decode_nt(const dllm_linear *h, const __half *X, int M, YT *Y, int nsplit, hipStream_t st) {
     const unsigned nbx = static_cast<unsigned>(h->Npad / (16 * NT));
     const int K = static_cast<int>(h->K), N = static_cast<int>(h->N);
     const int Np = static_cast<int>(h->Npad), gr = static_cast<int>(h->group);
@@ -1709,24 +1667,15 @@ int launch_decode_nt(const dllm_linear *h, const __half *X, int M, YT *Y, int ns
             }
         }
 #endif
-        if (next)
-            wq_decode_kernel<BITS, YT, MT, NT, false, 0, EXACT, kDecWaves, true><<<nbx, kDecWaves * 64, 0, st>>>(
-                X, M, K, h->wdec, h->sz, h->bias, Y, N, Np, gr, 1, nullptr, h->sf, next->wdec, next->sz, next->sf);
-        else
-            wq_decode_kernel<BITS, YT, MT, NT, false, 0, EXACT><<<nbx, kDecWaves * 64, 0, st>>>(
-                X, M, K, h->wdec, h->sz, h->bias, Y, N, Np, gr, 1, nullptr, h->sf);
+        wq_decode_kernel<BITS, YT, MT, NT, false, 0, EXACT><<<nbx, kDecWaves * 64, 0, st>>>(
+            X, M, K, h->wdec, h->sz, h->bias, Y, N, Np, gr, 1, nullptr, h->sf);
         DLLM_LAUNCH_CHECK();
         return DLLM_OK;
     }
     float *ws = device_workspace(st, static_cast<size_t>(nsplit) * M * h->Npad * sizeof(float));
     if (!ws) return DLLM_ERR_HIP;
-    const dim3 gd(nbx, static_cast<unsigned>(nsplit));
-    if (next)
-        wq_decode_kernel<BITS, YT, MT, NT, true, 0, EXACT, kDecWaves, true><<<gd, kDecWaves * 64, 0, st>>>(
-            X, M, K, h->wdec, h->sz, h->bias, Y, N, Np, gr, nsplit, ws, h->sf, next->wdec, next->sz, next->sf);
-    else
-        wq_decode_kernel<BITS, YT, MT, NT, true, 0, EXACT><<<gd, kDecWaves * 64, 0, st>>>(
-            X, M, K, h->wdec, h->sz, h->bias, Y, N, Np, gr, nsplit, ws, h->sf);
+    wq_decode_kernel<BITS, YT, MT, NT, true, 0, EXACT><<<dim3(nbx, static_cast<unsigned>(nsplit)), kDecWaves * 64, 0, st>>>(
+        X, M, K, h->wdec, h->sz, h->bias, Y, N, Np, gr, nsplit, ws, h->sf);
     DLLM_LAUNCH_CHECK();
     const size_t q = static_cast<size_t>(M) * (h->Npad / 4);
     const unsigned rb = static_cast<unsigned>(std::min<size_t>((q + 255) / 256, 4 * kCUs));
@@ -1736,22 +1685,20 @@ int launch_decode_nt(const dllm_linear *h, const __half *X, int M, YT *Y, int ns
 }
 
 template <int BITS, typename YT, int MT, int EXACT>
-int launch_decode_mt(const dllm_linear *h, const __half *X, int M, YT *Y, int nt, int nsplit, hipStream_t st,
-                     const dllm_linear *next) {
+int launch_decode_mt(const dllm_linear *h, const __half *X, int M, YT *Y, int nt, int nsplit, hipStream_t st) {
     switch (nt) {
-    case 2: return launch_decode_nt<BITS, YT, MT, 2, EXACT>(h, X, M, Y, nsplit, st, next);
-    case 4: return launch_decode_nt<BITS, YT, MT, 4, EXACT>(h, X, M, Y, nsplit, st, next);
-    default: return launch_decode_nt<BITS, YT, MT, 1, EXACT>(h, X, M, Y, nsplit, st, next);
+    case 2: return launch_decode_nt<BITS, YT, MT, 2, EXACT>(h, X, M, Y, nsplit, st);
+    case 4: return launch_decode_nt<BITS, YT, MT, 4, EXACT>(h, X, M, Y, nsplit, st);
+    default: return launch_decode_nt<BITS, YT, MT, 1, EXACT>(h, X, M, Y, nsplit, st);
     }
 }
 
 template <int BITS, typename YT, int EXACT>
-int launch_decode_x(const dllm_linear *h, const __half *X, size_t M, YT *Y, int nt, int nsplit, hipStream_t st,
-                    const dllm_linear *next) {
+int launch_decode_x(const dllm_linear *h, const __half *X, size_t M, YT *Y, int nt, int nsplit, hipStream_t st) {
     const int Mi = static_cast<int>(M);
-    if (M <= 16) return launch_decode_mt<BITS, YT, 1, EXACT>(h, X, Mi, Y, nt, nsplit, st, next);
-    if (M <= 32) return launch_decode_mt<BITS, YT, 2, EXACT>(h, X, Mi, Y, nt, nsplit, st, next);
-    return launch_decode_mt<BITS, YT, 4, EXACT>(h, X, Mi, Y, nt, nsplit, st, next);
+    if (M <= 16) return launch_decode_mt<BITS, YT, 1, EXACT>(h, X, Mi, Y, nt, nsplit, st);
+    if (M <= 32) return launch_decode_mt<BITS, YT, 2, EXACT>(h, X, Mi, Y, nt, nsplit, st);
+    return launch_decode_mt<BITS, YT, 4, EXACT>(h, X, Mi, Y, nt, nsplit, st);
 }
 
 #if DLLM_LAB
@@ -1778,13 +1725,8 @@ int ensure_decode_layout(const dllm_linear *h, hipStream_t) {
 }
 
 template <int BITS, typename YT>
-int launch_decode(const dllm_linear *h, const __half *X, size_t M, YT *Y, hipStream_t st,
-                  const dllm_linear *next = nullptr) {
+int launch_decode(const dllm_linear *h, const __half *X, size_t M, YT *Y, hipStream_t st) {
     if (const int rc = ensure_decode_layout(h, st)) return rc;
-    // the prefetch mirrors this launch's reads, so `next` must give the same grid and layouts
-    if (next && (next->K != h->K || next->Npad != h->Npad || next->bits != h->bits || next->group != h->group ||
-                 use_exact(next) != use_exact(h) || !next->wdec))
-        next = nullptr;
     int nt, nsplit;
     decode_policy(static_cast<int>(M), nt, nsplit);
 #if DLLM_LAB
@@ -1797,10 +1739,10 @@ int launch_decode(const dllm_linear *h, const __half *X, size_t M, YT *Y, hipStr
     // the column group must tile Npad (a multiple of 128)
     while (nt > 1 && h->Npad % (16 * nt)) nt /= 2;
     if (use_exact(h)) {
-        if (h->group == 64) return launch_decode_x<BITS, YT, 1>(h, X, M, Y, nt, nsplit, st, next);
-        return launch_decode_x<BITS, YT, 2>(h, X, M, Y, nt, nsplit, st, next);
+        if (h->group == 64) return launch_decode_x<BITS, YT, 1>(h, X, M, Y, nt, nsplit, st);
+        return launch_decode_x<BITS, YT, 2>(h, X, M, Y, nt, nsplit, st);
     }
-    return launch_decode_x<BITS, YT, 0>(h, X, M, Y, nt, nsplit, st, next);
+    return launch_decode_x<BITS, YT, 0>(h, X, M, Y, nt, nsplit, st);
 }
 
 // 3-stage-ring GEMM (rounded weights) with tile (32 MR) x (32 NW), K optionally split into nsplit slices.
@@ -2077,9 +2019,8 @@ int launch_prefill_auto(const dllm_linear *h, const __half *X, int M, YT *Y, hip
 }
 
 template <int BITS, typename YT>
-int launch_gemm_t(const dllm_linear *h, const __half *X, size_t M, YT *Y, hipStream_t st,
-                  const dllm_linear *next = nullptr) {
-    if (M <= static_cast<size_t>(kDecodeMaxM)) return launch_decode<BITS, YT>(h, X, M, Y, st, next);
+int launch_gemm_t(const dllm_linear *h, const __half *X, size_t M, YT *Y, hipStream_t st) {
+    if (M <= static_cast<size_t>(kDecodeMaxM)) return launch_decode<BITS, YT>(h, X, M, Y, st);
     return launch_prefill_auto<BITS, YT>(h, X, static_cast<int>(M), Y, st);
 }
 
@@ -2089,10 +2030,9 @@ int psample_fused(dllm_linear *h, const __half *Xh, int M, const PSampleEpi &ep,
 }
 
 template <int BITS>
-int launch_gemm(const dllm_linear *h, const __half *X, size_t M, void *Y, int y_dtype, hipStream_t st,
-                const dllm_linear *next = nullptr) {
-    if (y_dtype == DLLM_F32) return launch_gemm_t<BITS, float>(h, X, M, static_cast<float *>(Y), st, next);
-    return launch_gemm_t<BITS, __half>(h, X, M, static_cast<__half *>(Y), st, next);
+int launch_gemm(const dllm_linear *h, const __half *X, size_t M, void *Y, int y_dtype, hipStream_t st) {
+    if (y_dtype == DLLM_F32) return launch_gemm_t<BITS, float>(h, X, M, static_cast<float *>(Y), st);
+    return launch_gemm_t<BITS, __half>(h, X, M, static_cast<__half *>(Y), st);
 }
 
 void free_linear(dllm_linear *h) {
@@ -2308,11 +2248,6 @@ static int prepare_x(dllm_linear *h, const void *X, size_t M, int x_dtype, hipSt
 
 int dllm_linear_forward(dllm_linear_t h, const void *X, size_t M, int x_dtype, void *Y, int y_dtype,
                         dllm_stream_t stream) {
-    return dllm_linear_forward_prefetch(h, X, M, x_dtype, Y, y_dtype, nullptr, stream);
-}
-
-int dllm_linear_forward_prefetch(dllm_linear_t h, const void *X, size_t M, int x_dtype, void *Y, int y_dtype,
-                                 dllm_linear_t next, dllm_stream_t stream) {
     if (!h) return fail(DLLM_ERR_INVALID_PARAMS, "null handle");
     if ((x_dtype != DLLM_F32 && x_dtype != DLLM_F16) || (y_dtype != DLLM_F32 && y_dtype != DLLM_F16))
         return fail(DLLM_ERR_UNSUPPORTED, "dtype must be DLLM_F32 or DLLM_F16");
@@ -2325,9 +2260,9 @@ int dllm_linear_forward_prefetch(dllm_linear_t h, const void *X, size_t M, int x
     const __half *Xh = nullptr;
     if (const int rc = prepare_x(h, X, M, x_dtype, st, &Xh)) return rc;
     switch (h->bits) {
-    case 2: return launch_gemm<2>(h, Xh, M, Y, y_dtype, st, next);
-    case 4: return launch_gemm<4>(h, Xh, M, Y, y_dtype, st, next);
-    case 8: return launch_gemm<8>(h, Xh, M, Y, y_dtype, st, next);
+    case 2: return launch_gemm<2>(h, Xh, M, Y, y_dtype, st);
+    case 4: return launch_gemm<4>(h, Xh, M, Y, y_dtype, st);
+    case 8: return launch_gemm<8>(h, Xh, M, Y, y_dtype, st);
     default: return fail(DLLM_ERR_UNSUPPORTED, "bits");
     }
 }

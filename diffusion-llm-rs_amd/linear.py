@@ -50,11 +50,8 @@ class QuantLinear:
             _ptr(b), K, N, bits, group, int(precision), C.byref(h), _stream()))
         return cls(h, K, N, bits, group, precision)
 
-    def forward(self, x: torch.Tensor, out: torch.Tensor | None = None, out_dtype=torch.float16,
-                prefetch: "QuantLinear | None" = None) -> torch.Tensor:
-        """``forward(x) = x . W^ + b`` for x [M, K] (f16 or f32) -> [M, N].  ``prefetch``: the layer
-        that runs next in a chain (``dllm_linear_forward_prefetch``: at M <= 64 this call pulls that
-        layer's weights into L2 for the next call; bit-identical result)."""
+    def forward(self, x: torch.Tensor, out: torch.Tensor | None = None, out_dtype=torch.float16) -> torch.Tensor:
+        """``forward(x) = x . W^ + b`` for x [M, K] (f16 or f32) -> [M, N]."""
         if x.dim() != 2 or x.shape[1] != self.K:
             raise _lib.ShapeMismatch(f"x must be [M, {self.K}], got {tuple(x.shape)}")
         if not x.is_cuda or not x.is_contiguous():
@@ -66,11 +63,7 @@ class QuantLinear:
             out = torch.empty(M, self.N, dtype=out_dtype, device=x.device)
         xdt = _lib.F16 if x.dtype == torch.float16 else _lib.F32
         ydt = _lib.F16 if out.dtype == torch.float16 else _lib.F32
-        if prefetch is None:
-            check(_lib.load().dllm_linear_forward(self._h, _ptr(x), M, xdt, _ptr(out), ydt, _stream()))
-        else:
-            check(_lib.load().dllm_linear_forward_prefetch(self._h, _ptr(x), M, xdt, _ptr(out), ydt, prefetch._h,
-                                                           _stream()))
+        check(_lib.load().dllm_linear_forward(self._h, _ptr(x), M, xdt, _ptr(out), ydt, _stream()))
         return out
 
     __call__ = forward
@@ -146,10 +139,8 @@ class MixedPrecisionStack:
             self.layers.append(QuantLinear.from_weight(W, b, bits[i % len(bits)], group))
 
     def forward(self, x: torch.Tensor, out_dtype=torch.float16) -> torch.Tensor:
-        last = len(self.layers) - 1
         for i, layer in enumerate(self.layers):
-            x = layer(x, out_dtype=out_dtype if i == last else torch.float16,
-                      prefetch=self.layers[i + 1] if i < last else None)
+            x = layer(x, out_dtype=out_dtype if i == len(self.layers) - 1 else torch.float16)
         return x
 
     __call__ = forward

@@ -229,15 +229,6 @@ int dllm_linear_create_quantized_ex(const uint8_t *packed_codes, const float *sc
  * (same bound, different f32 summation order). */
 int dllm_linear_forward(dllm_linear_t h, const void *X, size_t M, int x_dtype, void *Y, int y_dtype,
                         dllm_stream_t stream);
-/* dllm_linear_forward for one layer of a chain (the layer loop of SimpleDiffusionModel::forward,
- * lib.rs:806-813): when the call takes the weight-streaming decode path (M <= 64) and `next` (may be
- * NULL) has the same K, N, bits, group and kernel family, every workgroup also loads the cache lines
- * of `next`'s weight codes and scales that the same workgroup of next's call (M unchanged) will read,
- * so `next` starts on weights already in its XCD's L2 instead of in HBM.  The result is
- * bit-identical to dllm_linear_forward; `next` is only read.  Other M, or a `next` of another shape:
- * exactly dllm_linear_forward. */
-int dllm_linear_forward_prefetch(dllm_linear_t h, const void *X, size_t M, int x_dtype, void *Y, int y_dtype,
-                                 dllm_linear_t next, dllm_stream_t stream);
 /* Export the quantized weights in canonical form (packed bitstream [K][N], scales [G][N], zps);
  * the codes are rebuilt from the device layout (the handle keeps no canonical copy). */
 int dllm_linear_export(dllm_linear_t h, uint8_t *packed_codes, float *scales, uint8_t *zps,

@@ -606,30 +606,6 @@ def test_linear_decode_first_call_in_capture(dllm, torch):
     ref.close()
 
 
-@pytest.mark.parametrize("M", [1, 7, 16, 33, 64, 65])
-@pytest.mark.parametrize("bits,group", [(4, 128), (4, 64), (2, 128), (8, 128)])
-def test_linear_forward_prefetch_bit_identical(dllm, torch, M, bits, group):
-    """dllm_linear_forward_prefetch: a chain of three layers with each call prefetching the next
-    layer's weights gives the bits of plain forward calls, on every decode configuration (M 1..64:
-    one tile, two token tiles, NT 4 x K-split 4) and past it (M 65: no prefetch); a `next` of another
-    shape (here the 1536-wide layer) is ignored."""
-    K, N = 1536, 1024
-    g = torch.Generator(device="cuda").manual_seed(31 + M + bits)
-    Ws = [0.02 * torch.randn(K, N, device="cuda", generator=g) for _ in range(3)]
-    lins = [dllm.QuantLinear.from_weight(W, None, bits, group) for W in Ws]
-    odd = dllm.QuantLinear.from_weight(0.02 * torch.randn(N, K, device="cuda", generator=g), None, bits, group)
-    X = torch.randn(M, K, device="cuda", generator=g).half()
-    for nxt in (lins[1], odd):
-        plain = lins[0](X, out_dtype=torch.float32)
-        pref = lins[0](X, out_dtype=torch.float32, prefetch=nxt)
-        assert torch.equal(plain, pref)
-    a = [lins[i](X) for i in range(3)]
-    b = [lins[i](X, prefetch=lins[(i + 1) % 3]) for i in range(3)]
-    assert all(torch.equal(p, q) for p, q in zip(a, b))
-    for lin in lins + [odd]:
-        lin.close()
-
-
 @pytest.mark.parametrize("M", [4096, 1800])
 def test_linear_horner_first_call_in_capture(dllm, torch, orc, M):
     """The forward contract: a handle's first call on a Horner grid (K = N = 4096, int4 g128; M 4096:
