@@ -121,6 +121,7 @@ SIGNATURES = {
     "dllm_p_sample": (INT, [P, P, P, P, S, S, INT, U64, U64, P, P]),
     "dllm_add_noise": (INT, [P, P, P, S, S, U64, U64, P, P, P]),
     "dllm_linear_forward_psample": (INT, [P, P, S, INT, P, P, S, INT, U64, U64, P, P, P]),
+    "dllm_linear_forward_psample_ex": (INT, [P, P, S, INT, P, P, S, INT, U64, U64, P, P, P, P]),
     "dllm_quantize_tensor_host": (INT, [P, S, U8, P, P, P]),
     "dllm_dequantize_tensor_host": (INT, [P, S, FL, FL, P]),
     "dllm_default_quantize_host": (INT, [P, S, INT, FL, I32, P]),

@@ -21,6 +21,7 @@ struct PSampleEpi {
     uint64_t seed, offset;
     float *x_prev;
     const float *noise;   // precomputed noise [M][N] (e.g. drawn on a side stream), or null: in-lane
+    __half *x_prev_h = nullptr;   // optional f16 copy of x_prev (RNE): the next step's first-layer X
 };
 
 namespace {
@@ -49,6 +50,12 @@ __device__ __forceinline__ void psample4(const PSampleEpi &e, int m, int n, int 
     o.z = (c1 * x.z + c2 * e2) + sd * z[2];
     o.w = (c1 * x.w + c2 * e3) + sd * z[3];
     *reinterpret_cast<float4 *>(e.x_prev + i) = o;
+    if (e.x_prev_h) {
+        union { __half h[4]; uint2 u; } pk;
+        pk.h[0] = __float2half_rn(o.x); pk.h[1] = __float2half_rn(o.y);
+        pk.h[2] = __float2half_rn(o.z); pk.h[3] = __float2half_rn(o.w);
+        *reinterpret_cast<uint2 *>(e.x_prev_h + i) = pk.u;
+    }
 }
 
 // Dequantizes the A fragment (8 f16) of substep s from a lane's slab words.

@@ -2270,6 +2270,14 @@ int dllm_linear_forward(dllm_linear_t h, const void *X, size_t M, int x_dtype, v
 int dllm_linear_forward_psample(dllm_linear_t h, const void *X, size_t M, int x_dtype, const float *x_t,
                                 const float *coef, size_t rows_per_sample, int add_noise, uint64_t seed,
                                 uint64_t offset, const float *noise, float *x_prev, dllm_stream_t stream) {
+    return dllm_linear_forward_psample_ex(h, X, M, x_dtype, x_t, coef, rows_per_sample, add_noise, seed, offset,
+                                          noise, x_prev, nullptr, stream);
+}
+
+int dllm_linear_forward_psample_ex(dllm_linear_t h, const void *X, size_t M, int x_dtype, const float *x_t,
+                                   const float *coef, size_t rows_per_sample, int add_noise, uint64_t seed,
+                                   uint64_t offset, const float *noise, float *x_prev, void *x_prev_f16,
+                                   dllm_stream_t stream) {
     if (!h) return fail(DLLM_ERR_INVALID_PARAMS, "null handle");
     if (x_dtype != DLLM_F32 && x_dtype != DLLM_F16) return fail(DLLM_ERR_UNSUPPORTED, "x_dtype");
     if (M == 0) return DLLM_OK;
@@ -2278,8 +2286,8 @@ int dllm_linear_forward_psample(dllm_linear_t h, const void *X, size_t M, int x_
     if (h->N % 4) return fail(DLLM_ERR_UNSUPPORTED, "fused p_sample needs N % 4 == 0");
     if (offset % 4) return fail(DLLM_ERR_INVALID_PARAMS, "offset must be a multiple of 4");
     if ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(x_t) | reinterpret_cast<uintptr_t>(x_prev) |
-         reinterpret_cast<uintptr_t>(noise)) & 15)
-        return fail(DLLM_ERR_INVALID_PARAMS, "X, x_t, noise and x_prev must be 16-byte aligned");
+         reinterpret_cast<uintptr_t>(noise) | reinterpret_cast<uintptr_t>(x_prev_f16)) & 15)
+        return fail(DLLM_ERR_INVALID_PARAMS, "X, x_t, noise, x_prev and x_prev_f16 must be 16-byte aligned");
     hipStream_t st = as_stream(stream);
     const __half *Xh = nullptr;
     if (const int rc = prepare_x(h, X, M, x_dtype, st, &Xh)) return rc;
@@ -2307,9 +2315,18 @@ int dllm_linear_forward_psample(dllm_linear_t h, const void *X, size_t M, int x_
             DLLM_LAUNCH_CHECK();
             coef = rc3;
         }
-        return dllm_p_sample(x_t, eps, noise, coef, M, h->N, add_noise, seed, offset, x_prev, stream);
+        if (const int prc = dllm_p_sample(x_t, eps, noise, coef, M, h->N, add_noise, seed, offset, x_prev, stream))
+            return prc;
+        if (x_prev_f16) {
+            const size_t n = M * h->N;
+            cast_f32_f16_kernel<<<grid_for(n / 4 + 1, 256, kCUs * 8), 256, 0, st>>>(x_prev, n,
+                                                                                     static_cast<__half *>(x_prev_f16));
+            DLLM_LAUNCH_CHECK();
+        }
+        return DLLM_OK;
     }
-    const PSampleEpi ep{x_t, coef, static_cast<int>(rows_per_sample), add_noise ? 1 : 0, seed, offset, x_prev, noise};
+    const PSampleEpi ep{x_t, coef, static_cast<int>(rows_per_sample), add_noise ? 1 : 0, seed, offset, x_prev, noise,
+                        static_cast<__half *>(x_prev_f16)};
     switch (h->bits) {
     case 2: return psample_fused<2>(h, Xh, (int)M, ep, st);
     case 4: return psample_fused<4>(h, Xh, (int)M, ep, st);

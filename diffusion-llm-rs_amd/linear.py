@@ -70,11 +70,13 @@ class QuantLinear:
 
     def forward_psample(self, x: torch.Tensor, x_t: torch.Tensor, coef: torch.Tensor, rows_per_sample: int,
                         add_noise: bool, seed: int, offset: int, out: Optional[torch.Tensor] = None,
-                        noise: Optional[torch.Tensor] = None) -> torch.Tensor:
+                        noise: Optional[torch.Tensor] = None, out16: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Output layer of the denoiser fused with p_sample (diffuse-llm-rs/src/lib.rs:1188-1212):
         eps = x . W^ + b (f32) and x_prev = (c1 x_t + c2 eps) + std * noise in the GEMM epilogue.
         x [M, K] f16/f32, x_t / out f32 [M, N], coef f32 [M / rows_per_sample, 3] (device); noise
-        f32 [M, N] precomputed, or None to draw stream elements offset + m N + n in the epilogue."""
+        f32 [M, N] precomputed, or None to draw stream elements offset + m N + n in the epilogue.
+        ``out16`` (f16 [M, N], optional): also receives x_prev rounded to f16 from the same epilogue
+        (dllm_linear_forward_psample_ex), the next step's first-layer input."""
         if x.dim() != 2 or x.shape[1] != self.K:
             raise _lib.ShapeMismatch(f"x must be [M, {self.K}], got {tuple(x.shape)}")
         x = _dev(x) if (not x.is_cuda or not x.is_contiguous()) else x
@@ -85,10 +87,13 @@ class QuantLinear:
             raise _lib.ShapeMismatch(f"x_t must be f32 [{M}, {self.N}]")
         out = torch.empty_like(x_t) if out is None else out
         xdt = _lib.F16 if x.dtype == torch.float16 else _lib.F32
-        check(_lib.load().dllm_linear_forward_psample(self._h, _ptr(x), M, xdt, _ptr(x_t), _ptr(coef),
-                                                      int(rows_per_sample), int(bool(add_noise)), int(seed),
-                                                      int(offset), None if noise is None else _ptr(noise),
-                                                      _ptr(out), _stream()))
+        if out16 is not None and (tuple(out16.shape) != (M, self.N) or out16.dtype != torch.float16):
+            raise _lib.ShapeMismatch(f"out16 must be f16 [{M}, {self.N}]")
+        check(_lib.load().dllm_linear_forward_psample_ex(self._h, _ptr(x), M, xdt, _ptr(x_t), _ptr(coef),
+                                                         int(rows_per_sample), int(bool(add_noise)), int(seed),
+                                                         int(offset), None if noise is None else _ptr(noise),
+                                                         _ptr(out), None if out16 is None else _ptr(out16),
+                                                         _stream()))
         return out
 
     def export(self):

@@ -358,6 +358,14 @@ int dllm_add_noise(const float *x0, const float *noise, const float *coef, size_
 int dllm_linear_forward_psample(dllm_linear_t h, const void *X, size_t M, int x_dtype, const float *x_t,
                                 const float *coef, size_t rows_per_sample, int add_noise, uint64_t seed,
                                 uint64_t offset, const float *noise, float *x_prev, dllm_stream_t stream);
+/* The same, also writing x_prev rounded to f16 (RNE, the cast dllm_linear_forward applies to an f32
+ * X) into x_prev_f16 (device [M][N], 16-byte aligned; NULL = none) from the same epilogue: the next
+ * denoise step's first layer takes it as its f16 input instead of casting x_prev again
+ * (DiffuseLLM::sample's x = x_prev hand-off, lib.rs:917-920). */
+int dllm_linear_forward_psample_ex(dllm_linear_t h, const void *X, size_t M, int x_dtype, const float *x_t,
+                                   const float *coef, size_t rows_per_sample, int add_noise, uint64_t seed,
+                                   uint64_t offset, const float *noise, float *x_prev, void *x_prev_f16,
+                                   dllm_stream_t stream);
 
 /* ---- host-slice variants (synchronous; stage through device memory; not graph-capturable) ----
  * The literal shapes of the reference's Rust signatures, for callers holding host slices. */

@@ -109,6 +109,13 @@ def test_linear_psample_fused_bit_identical(dllm, cuda, M, K, N, rps, precision)
     xt2 = xt.clone()
     lin.forward_psample(X, xt2, coef, rps, flag, seed=5, offset=16, out=xt2)
     assert torch.equal(xt2.view(torch.int32), ref.view(torch.int32))
+    # with the f16 copy of x_prev (dllm_linear_forward_psample_ex): the same f32 bits, and the f16
+    # copy is the RNE of them, as a first layer's own cast of an f32 X
+    h16 = torch.full((M, N), float("nan"), device="cuda", dtype=torch.float16)
+    xt3 = xt.clone()
+    lin.forward_psample(X, xt3, coef, rps, flag, seed=5, offset=16, out=xt3, out16=h16)
+    assert torch.equal(xt3.view(torch.int32), ref.view(torch.int32))
+    assert torch.equal(h16.view(torch.int16), ref.half().view(torch.int16))
     lin.close()
 
 
