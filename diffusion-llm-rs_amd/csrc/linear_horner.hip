@@ -40,9 +40,6 @@ constexpr int kHX = 256 * kBK * 2;            // X tile bytes per stage (32 KiB)
 constexpr int kHW = 8 * 1024;                 // 8 waves x 64 lanes x 16 B of weight words
 constexpr int kHG = 2048;                     // sz (1 KiB) + ratios (1 KiB), group-first stages
 constexpr int kHStage = kHX + kHW + kHG;      // 43008 B; 3 stages = 126 KiB
-// SPL (split rescale, lab A/B): each wave stages its own copy of its 32 columns' ratios (8 copies of
-// 128 B in a 1-KiB DMA) on a group's first stage: 50176 B per stage, 147 KiB for the ring.
-constexpr int kHStageS = kHX + kHW + 1024 + 8 * 1024;
 
 // One wave's stage burst: 4 X pieces (rows (8 i + wave) 8 ..) and its weight words, LDS-DMA
 // through buffer descriptors.  lds0 = this wave's first X destination; the next pieces follow at
@@ -77,10 +74,7 @@ __device__ __forceinline__ void horner_burst(__amdgpu_buffer_rsrc_t xr, uint32_t
 // MODE bit 0: the staggered schedule (product).  Lab ablations only (results wrong, timing only):
 // bit 1 no output stores; bit 2 no Horner rescale; bit 3 one dequant per k-step instead of four;
 // bit 4 one B fragment read per k-step instead of four; bit 5 no X DMA (weight words only); bit 6
-// no DMA at all.  Bit 7 (SPL, same results bit for bit): every wave stages its own copy of its
-// columns' ratios with the group's first stage, and the rescale is split: reps 0-3 are rescaled in the previous group's last
-// substep (which has no B reads or dequant), beside reps 4-7's MFMAs, and reps 4-7 in the group's
-// first substep, beside reps 0-3's MFMAs -- half the rescale VALU per substep where it was all in one.
+// no DMA at all.
 template <typename YT, int EPI, int MODE>
 __global__ void __launch_bounds__(512, 1)
 wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdev,
@@ -88,10 +82,7 @@ wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
                  const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad, int nbm, int nbn,
                  PSampleEpi epi) {
     constexpr bool STAG = MODE & 1;
-    constexpr bool SPL = (MODE & 128) != 0;
-    static_assert(!SPL || (STAG && (MODE & 4) == 0), "split rescale: staggered schedule with the rescale");
-    constexpr int kStage = SPL ? kHStageS : kHStage;
-    __shared__ __attribute__((aligned(16))) uint8_t smem[3 * kStage];
+    __shared__ __attribute__((aligned(16))) uint8_t smem[3 * kHStage];
 
     // XCD-aware bijective remap: blocks b and b + 8 share an XCD under round-robin dispatch, so the
     // 32 tiles an XCD holds at once are consecutive (2 row-blocks x 16 column-blocks at N = 4096).
@@ -121,14 +112,11 @@ wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
     // group data: wave 0 stages the {zp, scale} pairs, wave 1 the ratios (256 columns x 4 B each)
     const __amdgpu_buffer_rsrc_t gr =
         raw_rsrc(wave == 0 ? static_cast<const void *>(sz + n0) : static_cast<const void *>(hr + n0));
-    const bool has_g = wave < (SPL ? 1 : 2);   // SPL: wave 0 the {zp, scale} pairs, every wave its ratios
-    // SPL: 16-B chunk (lane & 7) of the wave's 32 ratio columns n0 + 32 wave .. (8 copies per DMA)
-    const __amdgpu_buffer_rsrc_t hrs = raw_rsrc(hr + n0 + wave * 32);
-    const uint32_t hoff = static_cast<uint32_t>((lane & 7) * 16);
+    const bool has_g = wave < 2;
     const uint32_t sbase = __builtin_amdgcn_readfirstlane(lds_addr(smem));
 
     auto stage = [&](int slot, int kt, bool gf) __attribute__((always_inline)) {
-        const uint32_t base = sbase + static_cast<uint32_t>(slot * kStage);
+        const uint32_t base = sbase + static_cast<uint32_t>(slot * kHStage);
         if constexpr ((MODE & 64) != 0) {
             // lab ablation: no DMA at all
         } else if constexpr ((MODE & 32) != 0) {   // lab ablation: the weight words only
@@ -140,9 +128,6 @@ wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
         if ((MODE & 64) == 0 && gf && has_g)
             blds16_asm(gr, wo, static_cast<uint32_t>((kt >> 1) * Npad * 4),
                        base + static_cast<uint32_t>(kHX + kHW + wave * 1024));
-        if (SPL && gf)
-            blds16_asm(hrs, hoff, static_cast<uint32_t>((kt >> 1) * Npad * 4),
-                       base + static_cast<uint32_t>(kHX + kHW + 1024 + wave * 1024));
     };
 
     float16_t acc[8];
@@ -165,22 +150,9 @@ wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
     ExactConsts ec;
     uint32_t w[4];
     float4 r4[4];
-    // SPL: r4 holds the next group's ratios from its previous substep on (1.0 before the first
-    // group, whose accumulator is 0)
-#pragma unroll
-    for (int qd = 0; qd < 4; ++qd) r4[qd] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
-    auto rescale = [&](int r) __attribute__((always_inline)) {
-#pragma unroll
-        for (int qd = 0; qd < 4; ++qd) {
-            acc[r][4 * qd + 0] *= r4[qd].x;
-            acc[r][4 * qd + 1] *= r4[qd].y;
-            acc[r][4 * qd + 2] *= r4[qd].z;
-            acc[r][4 * qd + 3] *= r4[qd].w;
-        }
-    };
     half8_t bA[8], bB[8], aA, aB;
     auto sub = [&](const uint8_t *sb, half8_t (&bc)[8], half8_t (&bn)[8], const half8_t &ac, half8_t &an, int j,
-                   bool gf, bool pre = false) __attribute__((always_inline)) {
+                   bool gf) __attribute__((always_inline)) {
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_setprio(1);
         if (j < 3) {
@@ -189,39 +161,7 @@ wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
             else an = dequant_exact<4>(w, j + 1, ec);
         }
         const half8_t (&bu)[8] = (MODE & 16) ? bA : bc;
-        if (SPL && gf && j == 0) {
-            // reps 0-3 were rescaled in the previous substep; 4-7 now, beside 0-3's MFMAs
-#pragma unroll
-            for (int r = 4; r < 8; ++r) rescale(r);
-#pragma unroll
-            for (int r = 0; r < 8; ++r) acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bu[r], acc[r], 0, 0, 0);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-            }
-        } else if (SPL && pre) {
-            // the group's last substep (no B reads, no dequant): reps 0-3 get the next group's
-            // ratio right after their last MFMA of this group, beside reps 2-7's MFMAs
-#pragma unroll
-            for (int r = 0; r < 8; ++r) acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bu[r], acc[r], 0, 0, 0);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) rescale(r);
-            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
-            }
-            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-        } else if ((MODE & 4) == 0 && !SPL && gf && j == 0) {
+        if ((MODE & 4) == 0 && gf && j == 0) {
             // acc <- acc * r_g right before the group's first MFMA of each rep (scalar v_mul_f32:
             // the file is built without the SLP vectorizer)
 #pragma unroll
@@ -276,10 +216,8 @@ wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
     auto step = [&](int slot, int kt, auto gf_tag) __attribute__((always_inline)) {
         constexpr bool GF = decltype(gf_tag)::value;
         const bool issue = kt + 2 < nk;
-        // SPL: a group starts at k-step kt + 1 (its stage holds this wave's copy of its ratios)
-        const bool pre = SPL && !GF && kt + 1 < nk;
         if (!STAG && issue) stage((slot + 2) % 3, kt + 2, GF);   // kt + 2 opens a group iff kt does
-        const uint8_t *sb = smem + slot * kStage;
+        const uint8_t *sb = smem + slot * kHStage;
         {
             const uint4 v = *reinterpret_cast<const uint4 *>(sb + kHX + wave * 1024 + lane * 16);
             w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
@@ -288,11 +226,9 @@ wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
             half2_t nz, sc;
             split_sz(*reinterpret_cast<const uint32_t *>(sb + kHX + kHW + (wave * 32 + (lane & 31)) * 4), nz, sc);
             ec = exact_consts(nz);
-            if constexpr (!SPL) {
-                const float *rl = reinterpret_cast<const float *>(sb + kHX + kHW + 1024) + wave * 32 + 4 * hsel;
+            const float *rl = reinterpret_cast<const float *>(sb + kHX + kHW + 1024) + wave * 32 + 4 * hsel;
 #pragma unroll
-                for (int qd = 0; qd < 4; ++qd) r4[qd] = *reinterpret_cast<const float4 *>(rl + 8 * qd);
-            }
+            for (int qd = 0; qd < 4; ++qd) r4[qd] = *reinterpret_cast<const float4 *>(rl + 8 * qd);
         }
         read_b(bA, sb, 0);
         aA = dequant_exact<4>(w, 0, ec);
@@ -304,29 +240,11 @@ wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
             if (issue) stage((slot + 2) % 3, kt + 2, GF);
         }
         sub(sb, bA, bB, aA, aB, 2, GF);
-        if constexpr (SPL && !GF) {
-            // this wave's DMAs of stage kt + 1 landed (all but this step's burst of 5: kt + 2 does
-            // not open a group); its own ratio copy is readable without a barrier.  The last k-step
-            // (no next group) reads a stale slot and rescales by 1 instead: r4 is redefined on every
-            // path, so it is live only from here to the next group's first substep.
-            if (issue) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const float *rl = reinterpret_cast<const float *>(smem + ((slot + 1) % 3) * kStage + kHX + kHW + 1024 +
-                                                              wave * 1024) + 4 * hsel;
-#pragma unroll
-            for (int qd = 0; qd < 4; ++qd) {
-                const float4 v = *reinterpret_cast<const float4 *>(rl + 8 * qd);
-                r4[qd] = pre ? v : make_float4(1.0f, 1.0f, 1.0f, 1.0f);
-            }
-            sub(sb, bB, bA, aB, aA, 3, GF, true);
-        } else {
-            sub(sb, bB, bA, aB, aA, 3, GF);
-        }
+        sub(sb, bB, bA, aB, aA, 3, GF);
         // k-step kt + 1 must have landed; kt + 2's DMAs stay in flight across the barrier
         if (!grp_b) {
             if (issue) {
-                if (SPL && GF && has_g) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-                else if (GF && (has_g || SPL)) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                if (GF && has_g) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
                 else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
             } else {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -396,7 +314,7 @@ wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
     const bool full = (m0 + 256 <= M) && (n0 + 256 <= N) && (N % 4) == 0;
     if constexpr (std::is_same<YT, __half>::value) {
         if (full) {   // coalesced 16-B row stores through the drained ring (2 passes of 128 rows)
-            store_tile_f16_lds<8, 8>(smem, 3 * kStage, acc, bv, Y, N, m0, n0, wave, lane);
+            store_tile_f16_lds<8, 8>(smem, 3 * kHStage, acc, bv, Y, N, m0, n0, wave, lane);
             return;
         }
     }
@@ -795,11 +713,6 @@ int launch_horner_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
         else if (a.lab == 7) launch_horner_t<3 | 4 | 8 | 16>(a, y_f32, st);
         else if (a.lab == 8) launch_horner_t<3 | 32>(a, y_f32, st);
         else launch_horner_t<3 | 64>(a, y_f32, st);
-        DLLM_LAUNCH_CHECK();
-        return DLLM_OK;
-    }
-    if (a.lab == 10) {   // lab A/B: split rescale (bit-identical to the product)
-        launch_horner_t<1 | 128>(a, y_f32, st);
         DLLM_LAUNCH_CHECK();
         return DLLM_OK;
     }
