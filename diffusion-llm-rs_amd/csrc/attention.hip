@@ -590,6 +590,15 @@ kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
             __builtin_amdgcn_sched_group_barrier(0x002, 5, 1);
         }
+        // Keep the softmax in region 1: without these the compiler sinks the 32 exponentials (and
+        // their fmas) past the O-rescale branch into region 2, where they run back to back ahead of
+        // the P V MFMAs while region 1's S^T MFMAs go without VALU fillers.
+        if constexpr (!(LAB & 1) && !(LAB & 512)) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(st[u][r]));
+        }
         if constexpr (STAG) raw_barrier();   // the half-block barrier
         // ---- rescale O rows by their query's alpha, only if some query's max moved ----
         if (!(LAB & 1) && !__all(alpha == 1.0f)) {
@@ -1006,6 +1015,9 @@ extern "C" int dllm_kv_attention(const void *Q, const uint8_t *Kq, const float *
 #undef DLLM_ALAB6
         case 302:   // the product without the region-2 priority (A/B; bit-identical)
             kv_attention5_kernel<256, false><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh);
+            break;
+        case 612:   // the product without the region-1 softmax pins (A/B; bit-identical)
+            kv_attention5_kernel<512, false><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh);
             break;
         case 198:   // the staggered schedule (A/B; bit-identical)
             kv_attention5_kernel<0, true><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh);
