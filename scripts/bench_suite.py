@@ -28,10 +28,17 @@ HBM = 8.0e12
 PEAK = 2.5e15
 
 
-def timed(fn, reps=20, warm=5):
+def timed(fn, reps=20, warm=5, warm_s=0.0):
+    """Mean seconds per call over ``reps`` calls, after ``warm`` untimed calls and, with ``warm_s``,
+    untimed calls of the same op until that many seconds have passed (the clocks ramp under load,
+    as in bench.py's pre-warm)."""
     for _ in range(warm):
         fn()
     torch.cuda.synchronize()
+    t0 = time.time()
+    while time.time() - t0 < warm_s:
+        fn()
+        torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
@@ -73,7 +80,7 @@ def c2():
     for M in (2048, 4096):
         X = torch.randn(M, K, device=dev).half()
         Y = torch.empty(M, N, dtype=torch.float16, device=dev)
-        s = timed(lambda: lin(X, out=Y))
+        s = timed(lambda: lin(X, out=Y), warm_s=0.2)
         b = K * N // 2 + (K // 128) * N * 5 + M * K * 2 + M * N * 2
         emit(config=f"C2 int4 g128 dequant+GEMM M={M} K=N=4096", us=round(s * 1e6, 1),
              tflops=round(2 * M * N * K / s / 1e12, 1), mfma_frac=round(2 * M * N * K / s / PEAK, 3),
@@ -135,7 +142,7 @@ def c4():
     emit(config="C4 KV quantize (K and V per tensor, int4 packed) S8192 H32 D128", us=round(s * 1e6, 1),
          GBs_algorithmic=round(2 * (4 * n + n / 2) / s / 1e9, 1))
     e = kvq()
-    s = timed(lambda: d.kv_attention(Q, e.keys, e.values), reps=5, warm=2)
+    s = timed(lambda: d.kv_attention(Q, e.keys, e.values), reps=10, warm=2, warm_s=0.3)
     fl = 4 * S * S * H * D
     emit(config="C4 int4 dequant-attention S8192 H32 D128", ms=round(s * 1e3, 3),
          tflops=round(fl / s / 1e12, 1), mfma_frac=round(fl / s / PEAK, 3))
