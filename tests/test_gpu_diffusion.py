@@ -174,11 +174,14 @@ def test_denoise_loop_vs_torch_f32(dllm, cuda, orc):
     assert rel <= 2e-3, rel
 
 
-def test_denoise_loop_overlap_bit_identical(dllm, cuda):
-    """The side-stream schedule (noise drawn ahead, KV update concurrent) gives the same bits as the
-    serial loop, and the KV cache ends in the same state."""
+@pytest.mark.parametrize("M", [48, 192])
+def test_denoise_loop_overlap_bit_identical(dllm, cuda, M):
+    """The overlapped schedule (KV update on the side stream; the last layer's epilogue also writes
+    x_prev in f16 for the next step's first layer -- from the fused epilogue at M 192, from the
+    p_sample + cast path at M 48) gives the same bits as the serial loop, and the KV cache ends in
+    the same state."""
     import torch
-    d, M, L, steps = 256, 192, 2, 5
+    d, L, steps = 256, 2, 5
     g = torch.Generator(device="cuda").manual_seed(4)
     layers = [dllm.QuantLinear.from_weight(0.04 * torch.randn(d, d, device="cuda", generator=g), None, 4, 128)
               for _ in range(L)]
