@@ -34,9 +34,10 @@ sys.path.insert(0, str(ROOT))
 PEAK_F16_TFLOPS = 2500.0   # MI355X dense f16/bf16 MFMA (MI355X_MICROARCH.md chip table)
 PEAK_HBM_GBS = 8000.0      # HBM3E spec
 # Revision tag of the default prefill GEMM kernel; a PMC record's traffic is quoted only when its
-# config carries the same tag (r03-horner: wq_horner_kernel of linear_horner.hip, the 256 x 256
-# Horner-form exact kernel with one DMA burst per stage and the LDS-staged coalesced f16 store).
-GEMM_REV = "r03-horner"
+# config carries the same tag (r03-horner-nt: wq_horner_kernel of linear_horner.hip, the 256 x 256
+# Horner-form exact kernel with one DMA burst per stage and the LDS-staged coalesced f16 store,
+# written with non-temporal 16-B stores).
+GEMM_REV = "r03-horner-nt"
 
 
 def parse():

@@ -24,6 +24,10 @@ struct PSampleEpi {
     __half *x_prev_h = nullptr;   // optional f16 copy of x_prev (RNE): the next step's first-layer X
 };
 
+#ifndef DLLM_NT_STORE
+#define DLLM_NT_STORE 1
+#endif
+
 namespace {
 
 constexpr int kBM = 256, kBN = 128, kBK = 64, kThreads = 256;
@@ -256,7 +260,13 @@ __device__ __forceinline__ void store_tile_f16_lds(uint8_t *img, int cap, const 
         for (int t0 = wave * kRowsPerInst; t0 < nrows; t0 += NW * kRowsPerInst) {
             const int t = t0 + lane / kCpr;
             const uint4 v = *reinterpret_cast<const uint4 *>(img + t * kRowB + ((c ^ (t & (kCpr - 1))) * 16));
+#if DLLM_NT_STORE   // non-temporal (streaming) Y stores: 1-2 % on the 4096^3 / 2048 x 4096^2 GEMMs (profiles/r03_nt_store)
+            typedef unsigned int u4nt __attribute__((ext_vector_type(4)));
+            __builtin_nontemporal_store(u4nt{v.x, v.y, v.z, v.w},
+                                        reinterpret_cast<u4nt *>(Y + static_cast<size_t>(m0 + p0 + t) * N + n0 + 8 * c));
+#else
             *reinterpret_cast<uint4 *>(Y + static_cast<size_t>(m0 + p0 + t) * N + n0 + 8 * c) = v;
+#endif
         }
         __syncthreads();
     }
