@@ -10,6 +10,13 @@
 
 #include "dllm_quant.h"
 
+// Streaming (non-temporal) stores for the GEMMs' f16 tile rows (whole 512-B rows per instruction;
+// A/B builds: -DDLLM_NT_STORE=0).  Not for the dequantize outputs: there the same hint is 1.1-2.7x
+// slower (profiles/r03_nt_store/dequant_ab.jsonl).
+#ifndef DLLM_NT_STORE
+#define DLLM_NT_STORE 1
+#endif
+
 namespace dllm {
 
 // Thread-local error message behind dllm_last_error().

@@ -24,10 +24,6 @@ struct PSampleEpi {
     __half *x_prev_h = nullptr;   // optional f16 copy of x_prev (RNE): the next step's first-layer X
 };
 
-#ifndef DLLM_NT_STORE
-#define DLLM_NT_STORE 1
-#endif
-
 namespace {
 
 constexpr int kBM = 256, kBN = 128, kBK = 64, kThreads = 256;
