@@ -695,6 +695,36 @@ kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__
     if (hh == 0) sm.bcast[wave][ql] = vs / l_run;
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_wave_barrier();
+    if constexpr (!(LAB & (4096 | 32)) && !STAG) {
+        // The wave's 32 x 128 f16 tile goes through the drained K/V ring (every wave passed the loop's
+        // last barrier, so nothing reads it any more; rows padded to 272 B so the two half-waves'
+        // rows land 16 banks apart) and leaves as whole 256-B rows in 16-B lane pieces: 8 global
+        // stores per lane instead of 64 two-byte ones (guide T21).
+        static_assert(kWaves * 32 * kKRow * 2 <= sizeof(sm.k) + sizeof(sm.vt), "O staging must fit the K/V ring");
+        _Float16 *tile = reinterpret_cast<_Float16 *>(&sm) + wave * 32 * kKRow;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const float4 inv = *reinterpret_cast<const float4 *>(&sm.bcast[wave][8 * g + 4 * hh]);
+            const float iv[4] = {inv.x, inv.y, inv.z, inv.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int r = 8 * g + 4 * hh + i;
+#pragma unroll
+                for (int dt = 0; dt < kD / 32; ++dt)
+                    tile[r * kKRow + 32 * dt + ql] = static_cast<_Float16>(o[dt][4 * g + i] * iv[i]);
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+            const int c = it * 64 + lane, r = c >> 4, cc = c & 15;
+            if (q0 + r < S)
+                *reinterpret_cast<u32x4_t *>(O + (static_cast<size_t>(q0 + r) * H + h) * kD + 8 * cc) =
+                    *reinterpret_cast<const u32x4_t *>(tile + r * kKRow + 8 * cc);
+        }
+        return;
+    }
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
         const float4 inv = *reinterpret_cast<const float4 *>(&sm.bcast[wave][8 * g + 4 * hh]);
@@ -1015,6 +1045,9 @@ extern "C" int dllm_kv_attention(const void *Q, const uint8_t *Kq, const float *
 #undef DLLM_ALAB6
         case 302:   // the product without the region-2 priority (A/B; bit-identical)
             kv_attention5_kernel<256, false><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh);
+            break;
+        case 4196:   // the product with the round-2 epilogue, 64 two-byte stores per lane (A/B; bit-identical)
+            kv_attention5_kernel<4096, false><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh);
             break;
         case 612:   // the product without the region-1 softmax pins (A/B; bit-identical)
             kv_attention5_kernel<512, false><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh);

@@ -1,7 +1,8 @@
 """A/B of the dequant-attention schedules on config C4 (S 8192, 32 heads x 128, int4 KV), lab build,
 one process (DLLM_ATTN_LAB is read per call), interleaved rounds, HIP events: 0 = the product
 (v5 with s_setprio 1 over region 2), 302 = v5 without that priority, 198 = v5 with waves 4-7
-staggered by half a key block.  The outputs must be bit-identical.
+staggered by half a key block, 4196 = v5 with the round-2 epilogue (64 two-byte O stores per
+lane).  The outputs must be bit-identical.
 Also checks ragged S (partial key blocks / query tiles).  Measurement only."""
 import json
 import os
@@ -30,7 +31,7 @@ for S in (65, 200, 4160, 8003):
     e = d.QuantizedKVCacheEntry.new(K, V, 4)
     outs = [run(l, Q, e) for l in labs]
     ident[S] = all(torch.equal(outs[0], o) for o in outs[1:])
-S, H, D = 8192, 32, 128
+S, H, D = int(os.environ.get("AB_S", "8192")), 32, 128   # AB_S: timed sequence length
 torch.manual_seed(0)
 K = torch.randn(S, H, D, device="cuda"); V = torch.randn(S, H, D, device="cuda")
 Q = torch.randn(S, H, D, device="cuda").half()
