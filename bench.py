@@ -98,23 +98,25 @@ def cpu_baseline(K, N, bits, group, M, budget_s):
     t_rows = time.perf_counter() - t0
     t_step = t_deq + t_rows / rows * M
     extrap = "" if rows == M else f", extrapolated from {rows} rows"
-    # the same on the host cores of this job's share (the GPU box gives one GPU
-    # 16 CPUs; os.cpu_count() there shows the whole machine).
-    threads = max(1, min(16, os.cpu_count() or 1))
+    # the same on the host cores this process may run on (its affinity mask;
+    # os.cpu_count() on the GPU box shows the whole machine), capped at the job's 16-CPU share.
+    threads = host_threads()
     orc.sgemm_blocked(X[:256], What, b, nthreads=threads)
     t0 = time.perf_counter()
     orc.sgemm_blocked(X, What, b, nthreads=threads)
     t_mt = t_deq + time.perf_counter() - t0
     gf = 2.0 * M * K * N / 1e9
     all_cores = {"value": M / t_mt, "unit": "tok/s", "cores": threads,
-                 "sample": f"same path on {threads} threads, all {M} rows: {t_mt:.3f}s per step "
+                 "sample": f"same path on {threads} threads (affinity mask {len(os.sched_getaffinity(0))} CPUs, "
+                           f"capped at the job's 16), all {M} rows: {t_mt:.3f}s per step "
                            f"({gf / (t_mt - t_deq):.0f} GFLOP/s sgemm)"}
     return {"value": M / t_step, "unit": "tok/s", "cores": 1, "kind": "port",
             "sample": f"1 thread: a2 dequant of the {K}x{N} int{bits} g{group} weight ({t_deq:.3f}s, C restatement) "
                       f"+ blocked AVX2/FMA sgemm (6x16 micro-tile, KC 256, MC 72; matrixmultiply's class) + bias on "
                       f"{rows} of {M} rows ({t_rows:.2f}s, {2.0 * rows * K * N / t_rows / 1e9:.0f} GFLOP/s){extrap}; "
                       f"step {t_step:.3f}s",
-            "host_cpu": _cpu_model(), "nproc": os.cpu_count(), "all_cores": all_cores}
+            "host_cpu": _cpu_model(), "nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)),
+            "multi_thread": all_cores}
 
 
 def cpu_denoise_step(dm=4096, M=2048, L=12, bits=4, group=128):
@@ -132,7 +134,7 @@ def cpu_denoise_step(dm=4096, M=2048, L=12, bits=4, group=128):
     b = np.zeros(dm, np.float32)
     X = rng.standard_normal((M, dm)).astype(np.float32)
     res = {}
-    for threads in (1, max(1, min(16, os.cpu_count() or 1))):
+    for threads in (1, host_threads()):
         orc.sgemm_blocked(X[:64], What, b, nthreads=threads)
         t0 = time.perf_counter()
         orc.sgemm_blocked(X, What, b, nthreads=threads)
@@ -142,6 +144,12 @@ def cpu_denoise_step(dm=4096, M=2048, L=12, bits=4, group=128):
     res["sample"] = (f"one layer (a2 dequant + blocked AVX2 sgemm {M}x{dm}x{dm} + b) timed per thread count, "
                      f"x {L} layers = one denoise step (extrapolated; p_sample not timed)")
     return res
+
+
+def host_threads():
+    """Threads for the multi-threaded CPU baseline: the CPUs of this process's affinity mask
+    (os.sched_getaffinity), at most the 16 a one-GPU job is given."""
+    return max(1, min(16, len(os.sched_getaffinity(0))))
 
 
 def _cpu_model():
@@ -178,7 +186,8 @@ def denoise_loop(d, torch, dev, steps=50):
     A side figure next to `value`, timed with HIP events on the loop's stream."""
     dm, M, L = 4096, 2048, 12
     g = torch.Generator(device=dev).manual_seed(99)
-    layers = [d.QuantLinear.from_weight((0.5 / 64.0) * torch.randn(dm, dm, device=dev, generator=g), None, 4, 128)
+    layers = [d.QuantLinear.from_weight((0.5 / 64.0) * torch.randn(dm, dm, device=dev, generator=g), None, 4, 128,
+                                        prefill_only=True)   # M = 2048 only: no decode layout
               for _ in range(L)]
     cfg = d.DiffusionConfig(num_timesteps=steps, hidden_size=dm, num_layers=L)
     kv = d.KVCacheEntry.new(torch.randn(1, M, dm, device=dev, generator=g),

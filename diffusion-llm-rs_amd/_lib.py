@@ -93,6 +93,11 @@ SIGNATURES = {
     "dllm_quantize_params_from_extremes": (INT, [P, U8, P, P]),
     "dllm_quantize_tensor_with_params": (INT, [P, S, U8, INT, P, P, P]),
     "dllm_quantize_tensor_pair_with_params": (INT, [P, S, U8, U8, INT, P, P, P, P, P]),
+    "dllm_quantize_kv_workspace": (S, [S, S]),
+    "dllm_quantize_kv": (INT, [P, S, P, S, U8, U8, INT, P, P, P, P, P, P, P, P, P, S, P]),
+    "dllm_kv_extremes": (INT, [P, S, P, S, P, P, S, P]),
+    "dllm_quantize_kv_with_extremes": (INT, [P, S, P, S, P, U8, U8, INT, P, P, P, P, P, P, P, P, P]),
+    "dllm_bias_cast": (INT, [P, S, S, P, P, INT, P]),
     "dllm_adaptive_update": (INT, [P, S, P, P, S, P]),
     "dllm_adaptive_compute_params": (INT, [P, INT, U32, P, P]),
     "dllm_adaptive_quantize": (INT, [P, S, U32, P, INT, P, P]),
@@ -157,16 +162,12 @@ _lib = None
 
 
 def load(path: str | os.PathLike | None = None):
-    """Loads libdllm_hip.so (raises if absent: there is no CPU fallback).  DLLM_LIB=lab selects the
-    lab build, DLLM_LIB=<file> another build of the same ABI (measurement scripts only)."""
+    """Loads libdllm_hip.so (raises if absent: there is no CPU fallback).  No environment variable
+    is read: the product library is the one in lib/.  ``path`` loads another build of the same ABI
+    and returns it without installing it (``use`` installs one: measurement scripts only)."""
     global _lib
     if _lib is not None and path is None:
         return _lib
-    env = os.environ.get("DLLM_LIB")
-    if path is None and env == "lab":
-        path = LAB_LIB_PATH
-    elif path is None and env:      # measurement A/B: an explicit library file
-        path = env
     p = Path(path) if path else LIB_PATH
     if not p.exists():
         raise ImportError(f"{p} not built; run `python -c 'import __graft_entry__ as g; g.build()'` "
@@ -179,9 +180,17 @@ def load(path: str | os.PathLike | None = None):
         if hasattr(lib, name):
             fn = getattr(lib, name)
             fn.restype, fn.argtypes = res, args
-    if path is None or (env and str(path) in (env, str(LAB_LIB_PATH))):
+    if path is None:
         _lib = lib
     return lib
+
+
+def use(path: str | os.PathLike):
+    """Installs another build of the same ABI (the lab build, an A/B variant) as the library every
+    call of this process goes to.  Measurement scripts and the lab tests call it explicitly."""
+    global _lib
+    _lib = load(path)
+    return _lib
 
 
 def check(rc: int):

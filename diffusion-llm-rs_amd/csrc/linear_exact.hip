@@ -552,7 +552,7 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
     }
     const bool full = (m0 + kBMt <= M) && (n0 + kBNt <= N) && (N % 4) == 0;
     if constexpr (std::is_same<YT, __half>::value && KG == 1 && NW * 64 >= 256) {
-        if (full) {   // coalesced 16-B row stores through the drained ring
+        if (full && (N % 8) == 0) {   // coalesced 16-B row stores (16-B aligned rows) through the drained ring
             store_tile_f16_lds<NW, MR>(ring, static_cast<int>(sizeof(ring)), acc, bv, Y, N, m0, n0, wave, lane);
             return;
         }

@@ -313,7 +313,7 @@ wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
     }
     const bool full = (m0 + 256 <= M) && (n0 + 256 <= N) && (N % 4) == 0;
     if constexpr (std::is_same<YT, __half>::value) {
-        if (full) {   // coalesced 16-B row stores through the drained ring (2 passes of 128 rows)
+        if (full && (N % 8) == 0) {   // coalesced 16-B row stores (16-B aligned rows) through the drained ring (2 passes of 128 rows)
             store_tile_f16_lds<8, 8>(smem, 3 * kHStage, acc, bv, Y, N, m0, n0, wave, lane);
             return;
         }

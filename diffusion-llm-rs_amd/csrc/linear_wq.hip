@@ -60,9 +60,7 @@ struct dllm_linear {
     float *bias = nullptr;        // [Npad]
     float *hr = nullptr;          // [G + 1][Npad] Horner ratios s_{g-1} / s_g (Horner-form shapes with valid scales)
     int hstate = 0;               // Horner form: 0 not applicable, 1 valid (hr kept), 2 not valid for these scales
-    __half *xws = nullptr;        // f32 -> f16 staging for X
-    size_t xws_elems = 0;
-    std::mutex mu;
+    bool prefill_only = false;    // DLLM_LINEAR_PREFILL_ONLY: no decode layout; M <= 64 runs the prefill kernels
 #if DLLM_LAB   // measurement knobs of the lab build (dllm_linear_set_kernel_variant)
     uint32_t *w16 = nullptr;      // 16x16x32 prefill layout (wq_gemm16_kernel)
     int variant = -1;             // prefill schedule variant (-1: product policy)
@@ -375,6 +373,27 @@ __global__ void __launch_bounds__(256) cast_f32_f16_kernel(const float *__restri
     }
     for (size_t i = n4 * 4 + blockIdx.x * static_cast<size_t>(256) + threadIdx.x; i < n; i += stride)
         y[i] = __float2half_rn(x[i]);
+}
+
+// The epilogue of a reduced row-parallel partial (dllm_bias_cast): out[m][n] = y[m][n] + bias[n]
+// (f32 add, the reference's `+ &self.bias` after the dot, lib.rs:812), stored in f32 or RNE f16.
+template <typename YT>
+__global__ void __launch_bounds__(256) bias_cast_kernel(const float *__restrict__ y, size_t M, size_t N,
+                                                        const float *__restrict__ bias, YT *__restrict__ out,
+                                                        int vec) {
+    const size_t stride = static_cast<size_t>(gridDim.x) * 256;
+    const size_t t0 = blockIdx.x * static_cast<size_t>(256) + threadIdx.x;
+    if (vec) {   // N % 4 == 0 and 16-B aligned rows: 4 outputs per thread
+        const size_t q = N / 4, total = M * q;
+        for (size_t i = t0; i < total; i += stride) {
+            const size_t n = (i % q) * 4;
+            const float4 v = reinterpret_cast<const float4 *>(y)[i];
+            const float4 b = bias ? *reinterpret_cast<const float4 *>(bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+            store4<YT>(out + i * 4, v.x + b.x, v.y + b.y, v.z + b.z, v.w + b.w);
+        }
+        return;
+    }
+    for (size_t i = t0; i < M * N; i += stride) store1<YT>(out + i, y[i] + (bias ? bias[i % N] : 0.0f));
 }
 
 // Row coefficient table: out[m] = coef[m / rps] (3 floats each).
@@ -2020,7 +2039,7 @@ int launch_prefill_auto(const dllm_linear *h, const __half *X, int M, YT *Y, hip
 
 template <int BITS, typename YT>
 int launch_gemm_t(const dllm_linear *h, const __half *X, size_t M, YT *Y, hipStream_t st) {
-    if (M <= static_cast<size_t>(kDecodeMaxM)) return launch_decode<BITS, YT>(h, X, M, Y, st);
+    if (M <= static_cast<size_t>(kDecodeMaxM) && h->wdec) return launch_decode<BITS, YT>(h, X, M, Y, st);
     return launch_prefill_auto<BITS, YT>(h, X, static_cast<int>(M), Y, st);
 }
 
@@ -2038,14 +2057,15 @@ int launch_gemm(const dllm_linear *h, const __half *X, size_t M, void *Y, int y_
 void free_linear(dllm_linear *h) {
     if (!h) return;
     (void)hipFree(h->wdev); (void)hipFree(h->wdec); (void)hipFree(h->sz); (void)hipFree(h->sf);
-    (void)hipFree(h->bias); (void)hipFree(h->xws); (void)hipFree(h->hr);
+    (void)hipFree(h->bias); (void)hipFree(h->hr);
 #if DLLM_LAB
     (void)hipFree(h->w16);
 #endif
     delete h;
 }
 
-int check_shape(size_t K, size_t N, uint8_t bits, size_t group, int precision) {
+int check_shape(size_t K, size_t N, uint8_t bits, size_t group, int flags) {
+    const int precision = flags & ~DLLM_LINEAR_PREFILL_ONLY;
     if (bits != 2 && bits != 4 && bits != 8)
         return fail(DLLM_ERR_UNSUPPORTED, "linear layer supports bits in {2, 4, 8}");
     if (K == 0 || N == 0) return fail(DLLM_ERR_SHAPE_MISMATCH, "K and N must be >= 1");
@@ -2057,17 +2077,20 @@ int check_shape(size_t K, size_t N, uint8_t bits, size_t group, int precision) {
     return DLLM_OK;
 }
 
-int alloc_linear(size_t K, size_t N, uint8_t bits, size_t group, int precision, dllm_linear **out) {
+int alloc_linear(size_t K, size_t N, uint8_t bits, size_t group, int flags, dllm_linear **out) {
     dllm_linear *h = new (std::nothrow) dllm_linear();
     if (!h) return fail(DLLM_ERR_HIP, "out of host memory");
-    h->K = K; h->N = N; h->bits = bits; h->group = group; h->precision = precision;
+    h->K = K; h->N = N; h->bits = bits; h->group = group;
+    h->precision = flags & ~DLLM_LINEAR_PREFILL_ONLY;
+    h->prefill_only = (flags & DLLM_LINEAR_PREFILL_ONLY) != 0;
     h->Npad = (N + kBN - 1) / kBN * kBN;
     h->G = (K + group - 1) / group;
     (void)hipGetDevice(&h->device);
     auto A = [&](void **p, size_t bytes) { return hipMalloc(p, std::max<size_t>(bytes, 16)); };
     hipError_t e = hipSuccess;
     if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->wdev), h->Npad * K * bits / 8);
-    if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->wdec), h->Npad * ((K + 127) / 128) * 128 * bits / 8);
+    if (e == hipSuccess && !h->prefill_only)
+        e = A(reinterpret_cast<void **>(&h->wdec), h->Npad * ((K + 127) / 128) * 128 * bits / 8);
     if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->sz), h->G * h->Npad * 4);
     if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->sf), h->G * h->Npad * 4);
     if (e == hipSuccess) e = A(reinterpret_cast<void **>(&h->bias), h->Npad * 4);
@@ -2098,9 +2121,11 @@ int finish_linear(dllm_linear *h, const uint32_t *canon, const float *scales, co
     build_fragments16_kernel<<<gf, 256, 0, st>>>(canon, h->K, h->N, h->Npad, h->bits, h->w16);
     DLLM_LAUNCH_CHECK();
 #endif
-    dim3 gd(static_cast<unsigned>((h->Npad + 255) / 256), static_cast<unsigned>((h->K + 127) / 128));
-    build_decode_from_wdev_kernel<<<gd, 256, 0, st>>>(h->wdev, h->K, h->Npad, h->bits, h->wdec);
-    DLLM_LAUNCH_CHECK();
+    if (h->wdec) {
+        dim3 gd(static_cast<unsigned>((h->Npad + 255) / 256), static_cast<unsigned>((h->K + 127) / 128));
+        build_decode_from_wdev_kernel<<<gd, 256, 0, st>>>(h->wdev, h->K, h->Npad, h->bits, h->wdec);
+        DLLM_LAUNCH_CHECK();
+    }
     dim3 gs(static_cast<unsigned>((h->Npad + 255) / 256), static_cast<unsigned>(h->G));
     build_sz_kernel<<<gs, 256, 0, st>>>(scales, zps, h->G, h->N, h->Npad, h->sz);
     DLLM_LAUNCH_CHECK();
@@ -2221,28 +2246,37 @@ int dllm_linear_create_quantized(const uint8_t *packed_codes, const float *scale
                                            out, stream);
 }
 
-// f16 view of X: as given, or cast from f32 through the handle's workspace.
+// f16 view of X: as given, or cast from f32 through the per-(device, stream) staging workspace
+// (slot 3): calls on one stream run in order, so they can share it, and calls on distinct streams
+// never touch each other's (a handle keeps no mutable state).
 static int prepare_x(dllm_linear *h, const void *X, size_t M, int x_dtype, hipStream_t st, const __half **Xh) {
     *Xh = static_cast<const __half *>(X);
     if (x_dtype != DLLM_F32) return DLLM_OK;
-    std::lock_guard<std::mutex> lk(h->mu);
     const size_t need = M * h->K;
-    if (h->xws_elems < need) {
-        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        (void)hipStreamIsCapturing(st, &cs);
-        if (cs != hipStreamCaptureStatusNone)
-            return fail(DLLM_ERR_INVALID_PARAMS, "f32 X workspace must be grown before stream capture");
-        DLLM_HIP_TRY(hipStreamSynchronize(st));
-        (void)hipFree(h->xws);
-        h->xws = nullptr;
-        h->xws_elems = 0;
-        DLLM_HIP_TRY(hipMalloc(reinterpret_cast<void **>(&h->xws), need * sizeof(__half)));
-        h->xws_elems = need;
-    }
-    cast_f32_f16_kernel<<<grid_for(need / 4 + 1, 256, kCUs * 8), 256, 0, st>>>(static_cast<const float *>(X), need,
-                                                                                 h->xws);
+    __half *xs = reinterpret_cast<__half *>(device_workspace(st, need * sizeof(__half), 3));
+    if (!xs) return DLLM_ERR_HIP;
+    cast_f32_f16_kernel<<<grid_for(need / 4 + 1, 256, kCUs * 8), 256, 0, st>>>(static_cast<const float *>(X), need, xs);
     DLLM_LAUNCH_CHECK();
-    *Xh = h->xws;
+    *Xh = xs;
+    return DLLM_OK;
+}
+
+int dllm_bias_cast(const float *y, size_t M, size_t N, const float *bias, void *out, int out_dtype,
+                   dllm_stream_t stream) {
+    if (out_dtype != DLLM_F32 && out_dtype != DLLM_F16) return fail(DLLM_ERR_UNSUPPORTED, "dtype must be DLLM_F32 or DLLM_F16");
+    if (M == 0 || N == 0) return DLLM_OK;
+    if (!y || !out) return fail(DLLM_ERR_INVALID_PARAMS, "null pointer");
+    if (out_dtype == DLLM_F16 && static_cast<const void *>(y) == out)
+        return fail(DLLM_ERR_INVALID_PARAMS, "an f16 output cannot alias the f32 input");
+    const int vec = (N % 4 == 0) && ((reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(bias) |
+                                      reinterpret_cast<uintptr_t>(out)) & 15) == 0;
+    hipStream_t st = as_stream(stream);
+    const unsigned g = grid_for(vec ? M * N / 4 : M * N, 256, kCUs * 8);
+    if (out_dtype == DLLM_F32)
+        bias_cast_kernel<float><<<g, 256, 0, st>>>(y, M, N, bias, static_cast<float *>(out), vec);
+    else
+        bias_cast_kernel<__half><<<g, 256, 0, st>>>(y, M, N, bias, static_cast<__half *>(out), vec);
+    DLLM_LAUNCH_CHECK();
     return DLLM_OK;
 }
 
@@ -2379,12 +2413,12 @@ size_t dllm_linear_weight_bytes(dllm_linear_t h) {
 size_t dllm_linear_device_bytes(dllm_linear_t h) {
     if (!h) return 0;
     size_t b = h->Npad * h->K * h->bits / 8 + h->G * h->Npad * 8 + h->Npad * 4;   // wdev, sz + sf, bias
-    b += h->Npad * ((h->K + 127) / 128) * 128 * h->bits / 8;                       // decode layout
+    if (h->wdec) b += h->Npad * ((h->K + 127) / 128) * 128 * h->bits / 8;         // decode layout
     if (h->hr) b += (h->G + 1) * h->Npad * 4;                                         // Horner ratios (valid ones)
 #if DLLM_LAB
     b += h->Npad * h->K * h->bits / 8;
 #endif
-    return b + h->xws_elems * sizeof(__half);
+    return b;
 }
 
 #if DLLM_LAB

@@ -16,6 +16,10 @@ namespace {
 
 constexpr int kBlock = 256;
 
+#ifndef DLLM_QMAP_OCTET
+#define DLLM_QMAP_OCTET 0
+#endif
+
 // ---------------------------------------------------------------------------------------------
 // Octet load / store helpers
 // ---------------------------------------------------------------------------------------------
@@ -152,12 +156,12 @@ __device__ __forceinline__ void block_minmax(float &mx, float &mn, float *smem /
     }
 }
 
-__global__ void __launch_bounds__(kBlock) minmax_partial_kernel(const float *__restrict__ x, size_t n, size_t head,
-                                                                float2 *__restrict__ partials) {
-    __shared__ float smem[2 * kBlock / 64];
+// Block `b` of `nb` folds its grid-stride share of x into partials[b] = {max, min}.
+__device__ __forceinline__ void minmax_body(const float *__restrict__ x, size_t n, size_t head,
+                                            float2 *__restrict__ partials, unsigned b, unsigned nb, float *smem) {
     float mx = -INFINITY, mn = INFINITY;
-    const size_t gid = blockIdx.x * static_cast<size_t>(kBlock) + threadIdx.x;
-    const size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+    const size_t gid = b * static_cast<size_t>(kBlock) + threadIdx.x;
+    const size_t stride = static_cast<size_t>(nb) * kBlock;
     if (gid < head) { float v = x[gid]; mx = fmaxf(mx, v); mn = fminf(mn, v); }
     const size_t nv = (n - head) / 4;
     const float4 *x4 = reinterpret_cast<const float4 *>(x + head);
@@ -178,7 +182,13 @@ __global__ void __launch_bounds__(kBlock) minmax_partial_kernel(const float *__r
     const size_t tail0 = head + nv * 4;
     if (gid < n - tail0) { float v = x[tail0 + gid]; mx = fmaxf(mx, v); mn = fminf(mn, v); }
     block_minmax(mx, mn, smem);
-    if (threadIdx.x == 0) partials[blockIdx.x] = make_float2(mx, mn);
+    if (threadIdx.x == 0) partials[b] = make_float2(mx, mn);
+}
+
+__global__ void __launch_bounds__(kBlock) minmax_partial_kernel(const float *__restrict__ x, size_t n, size_t head,
+                                                                float2 *__restrict__ partials) {
+    __shared__ float smem[2 * kBlock / 64];
+    minmax_body(x, n, head, partials, blockIdx.x, gridDim.x, smem);
 }
 
 // (scale, zp) from the extremes exactly as quantization.rs:49-56.
@@ -329,6 +339,84 @@ __device__ __forceinline__ void quantize_fused_body(const float *__restrict__ x,
     }
 }
 
+
+// The same map with every load instruction one contiguous KiB: a wave takes chunks of 512 float4
+// (2048 values); lane l holds float4s l, l + 64, ..., l + 448 of the chunk (8 loads in flight),
+// codes its 4 values into a 4B-bit field and stores it at the field's place in the packed stream
+// (B = 8: 4 bytes, 4: 2, 2: 1; B = 1: the nibbles of lanes 2i and 2i + 1 make one byte).  Octets
+// past the last whole chunk (and the partial tail octet) go through quantize_fused_body's code.
+template <int B>
+__device__ __forceinline__ void store_quad(uint8_t *__restrict__ out, size_t f, uint32_t w, int lane) {
+    if constexpr (B == 8) {
+        *reinterpret_cast<uint32_t *>(out + f * 4) = w;
+    } else if constexpr (B == 4) {
+        *reinterpret_cast<uint16_t *>(out + f * 2) = static_cast<uint16_t>(w);
+    } else if constexpr (B == 2) {
+        out[f] = static_cast<uint8_t>(w);
+    } else {
+        const uint32_t other = static_cast<uint32_t>(__shfl_xor(static_cast<int>(w), 1, 64));
+        if ((lane & 1) == 0) out[f >> 1] = static_cast<uint8_t>(w | (other << 4));
+    }
+}
+
+template <int BA, int BB, bool kFast>
+__device__ __forceinline__ void quantize_coalesced_body(const float *__restrict__ x, size_t n,
+                                                        uint8_t *__restrict__ out_a, uint8_t *__restrict__ out_b,
+                                                        float sa, float za, float sb, float zb, unsigned b,
+                                                        unsigned nb) {
+    const float ra = 1.0f / sa, rb = BB ? 1.0f / sb : 0.0f;
+    constexpr uint32_t ha = (1u << BA) - 1u, hb = BB ? (1u << BB) - 1u : 0u;
+    constexpr int kWaves = kBlock / 64;
+    const int lane = threadIdx.x & 63;
+    const size_t nchunk = n / 2048;
+    const float4 *x4 = reinterpret_cast<const float4 *>(x);
+    const size_t W = static_cast<size_t>(nb) * kWaves;
+    for (size_t c = static_cast<size_t>(b) * kWaves + (threadIdx.x >> 6); c < nchunk; c += W) {
+        float4 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = x4[c * 512 + j * 64 + lane];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float e[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+            uint32_t wa = 0, wb = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                wa |= code_of(div_scale<kFast>(e[i], sa, ra) + za, ha) << (i * BA);   // :61-64
+                if constexpr (BB != 0) wb |= code_of(div_scale<kFast>(e[i], sb, rb) + zb, hb) << (i * BB);
+            }
+            const size_t f = c * 512 + j * 64 + lane;
+            store_quad<BA>(out_a, f, wa, lane);
+            if constexpr (BB != 0) store_quad<BB>(out_b, f, wb, lane);
+        }
+    }
+    // the octets after the last whole chunk, then the partial tail octet
+    const size_t nfull = n / 8;
+    const size_t stride = static_cast<size_t>(nb) * kBlock;
+    for (size_t o = nchunk * 256 + b * static_cast<size_t>(kBlock) + threadIdx.x; o < nfull; o += stride) {
+        const float4 p0 = x4[2 * o], p1 = x4[2 * o + 1];
+        const float e[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+        uint32_t ca[8], cb[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            ca[i] = code_of(div_scale<kFast>(e[i], sa, ra) + za, ha);
+            if constexpr (BB != 0) cb[i] = code_of(div_scale<kFast>(e[i], sb, rb) + zb, hb);
+        }
+        store_packed<BA>(out_a, o, ca);
+        if constexpr (BB != 0) store_packed<BB>(out_b, o, cb);
+    }
+    if (b == 0 && threadIdx.x == 0 && n % 8) {
+        const int cnt = static_cast<int>(n - nfull * 8);
+        uint32_t ca[8] = {0, 0, 0, 0, 0, 0, 0, 0}, cb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int i = 0; i < cnt; ++i) {
+            const float v = x[nfull * 8 + i];
+            ca[i] = code_of(div_scale<kFast>(v, sa, ra) + za, ha);
+            if constexpr (BB != 0) cb[i] = code_of(div_scale<kFast>(v, sb, rb) + zb, hb);
+        }
+        store_codes(out_a, nfull, cnt, ca, BA, true, false);
+        if constexpr (BB != 0) store_codes(out_b, nfull, cnt, cb, BB, true, false);
+    }
+}
+
 // quantize_tensor (and the pair of widths of KVCacheEntry::update) after minmax_partial_kernel:
 // x 16-B aligned, packed codes (out 8-B aligned); block 0 publishes the params.
 template <int BA, int BB>
@@ -346,10 +434,98 @@ __global__ void __launch_bounds__(kBlock) quantize_fused_kernel(const float *__r
         params_a[0] = sa; params_a[1] = za;
         if constexpr (BB != 0) { params_b[0] = sb; params_b[1] = zb; }
     }
+#if DLLM_QMAP_OCTET   // A/B build: the round-3 octet-per-thread loads (two 32-B-strided float4 per lane)
     if (markstein_ok(sa) && (BB == 0 || markstein_ok(sb)))
         quantize_fused_body<BA, BB, true>(x, n, out_a, out_b, sa, za, sb, zb);
     else
         quantize_fused_body<BA, BB, false>(x, n, out_a, out_b, sa, za, sb, zb);
+#else
+    if (markstein_ok(sa) && (BB == 0 || markstein_ok(sb)))
+        quantize_coalesced_body<BA, BB, true>(x, n, out_a, out_b, sa, za, sb, zb, blockIdx.x, gridDim.x);
+    else
+        quantize_coalesced_body<BA, BB, false>(x, n, out_a, out_b, sa, za, sb, zb, blockIdx.x, gridDim.x);
+#endif
+}
+
+// ---------------------------------------------------------------------------------------------
+// Both tensors of one KV-cache quantization (QuantizedKVCacheEntry::new, quantization.rs:140-157,
+// and KVCacheEntry::update's two widths, lib.rs:241-276) as a few launches of one job kernel.  The
+// blocks of a launch are dealt round-robin to its jobs (block i -> job i % jobs), so a map job
+// whose x still sits in the Infinity Cache (read by the previous launch's min/max) runs beside a
+// min/max job streaming the other tensor from HBM:
+//   min/max K  |  map K (params folded from K's partials) + min/max V  |  map V.
+// A map job takes its extremes from min/max partials, or from {-min, max} already reduced over
+// the ranks of a head-sharded cache (dllm_quantize_kv_with_extremes).
+// ---------------------------------------------------------------------------------------------
+struct MapJob {
+    const float *x;
+    size_t n;
+    uint8_t *out_a, *out_b;
+    float *params_a, *params_b;
+    const float2 *partials;   // extremes from these min/max partials (np of them) ...
+    int np;
+    const float *red;         // ... or from {-min, max} (red != nullptr)
+};
+struct MinmaxJob {
+    const float *x;
+    size_t n, head;
+    float2 *partials;
+    unsigned nb;              // blocks (= partials written)
+};
+struct KVJobs {
+    MapJob map[2];
+    MinmaxJob mm[2];
+    int nmap, nmm;
+    unsigned nbq;             // blocks per map job
+};
+
+template <int BA, int BB>
+__global__ void __launch_bounds__(kBlock) kv_jobs_kernel(const KVJobs J) {
+    __shared__ float smem[2 * kBlock / 64];
+    const int jobs = J.nmap + J.nmm;
+    const int role = static_cast<int>(blockIdx.x % jobs);
+    const unsigned idx = blockIdx.x / jobs;
+    if (role >= J.nmap) {
+        const MinmaxJob &m = J.mm[role - J.nmap];
+        if (idx < m.nb) minmax_body(m.x, m.n, m.head, m.partials, idx, m.nb, smem);
+        return;
+    }
+    const MapJob &q = J.map[role];
+    if (idx >= J.nbq) return;
+    float mx, mn, sa, za, sb = 1.0f, zb = 0.0f;
+    if (q.red) {
+        mn = -q.red[0];
+        mx = q.red[1];
+    } else {
+        fold_partials(q.partials, q.np, smem, mx, mn);
+    }
+    params_of(mx, mn, BA, sa, za);
+    if constexpr (BB != 0) params_of(mx, mn, BB, sb, zb);
+    if (idx == 0 && threadIdx.x == 0) {
+        q.params_a[0] = sa; q.params_a[1] = za;
+        if constexpr (BB != 0) { q.params_b[0] = sb; q.params_b[1] = zb; }
+    }
+    if (markstein_ok(sa) && (BB == 0 || markstein_ok(sb)))
+        quantize_coalesced_body<BA, BB, true>(q.x, q.n, q.out_a, q.out_b, sa, za, sb, zb, idx, J.nbq);
+    else
+        quantize_coalesced_body<BA, BB, false>(q.x, q.n, q.out_a, q.out_b, sa, za, sb, zb, idx, J.nbq);
+}
+
+// {-min_K, max_K, -min_V, max_V} from the two tensors' min/max partials (dllm_kv_extremes).
+__global__ void __launch_bounds__(kBlock) kv_red_kernel(const float2 *__restrict__ pk, int nk,
+                                                        const float2 *__restrict__ pv, int nv, float *__restrict__ red) {
+    __shared__ float smem[2 * kBlock / 64];
+    float mx, mn;
+    fold_partials(pk, nk, smem, mx, mn);
+    if (threadIdx.x == 0) { red[0] = -mn; red[1] = mx; }
+    __syncthreads();
+    fold_partials(pv, nv, smem, mx, mn);
+    if (threadIdx.x == 0) { red[2] = -mn; red[3] = mx; }
+}
+
+// Params of width `bits` from {-min, max} (the generic fallback of dllm_quantize_kv_with_extremes).
+__global__ void params_from_red_kernel(const float *__restrict__ red, int bits, float *__restrict__ params) {
+    if (threadIdx.x == 0) write_params(red[1], -red[0], bits, params);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -737,6 +913,46 @@ inline int launch_fused(const float *x, size_t n, const float2 *partials, int np
     }
 }
 
+template <int BA>
+int launch_kv_jobs_b(const KVJobs &J, int bb, unsigned grid, hipStream_t st) {
+    switch (bb) {
+    case 0: kv_jobs_kernel<BA, 0><<<grid, kBlock, 0, st>>>(J); break;
+    case 1: kv_jobs_kernel<BA, 1><<<grid, kBlock, 0, st>>>(J); break;
+    case 2: kv_jobs_kernel<BA, 2><<<grid, kBlock, 0, st>>>(J); break;
+    case 4: kv_jobs_kernel<BA, 4><<<grid, kBlock, 0, st>>>(J); break;
+    default: kv_jobs_kernel<BA, 8><<<grid, kBlock, 0, st>>>(J); break;
+    }
+    DLLM_LAUNCH_CHECK();
+    return DLLM_OK;
+}
+
+// One launch of kv_jobs_kernel: every job gets `per` blocks (map jobs J.nbq, min/max jobs their nb).
+int launch_kv_jobs(KVJobs J, int ba, int bb, hipStream_t st) {
+    unsigned per = J.nmap ? J.nbq : 0;
+    for (int i = 0; i < J.nmm; ++i) per = std::max(per, J.mm[i].nb);
+    const unsigned grid = per * static_cast<unsigned>(J.nmap + J.nmm);
+    switch (ba) {
+    case 1: return launch_kv_jobs_b<1>(J, bb, grid, st);
+    case 2: return launch_kv_jobs_b<2>(J, bb, grid, st);
+    case 4: return launch_kv_jobs_b<4>(J, bb, grid, st);
+    default: return launch_kv_jobs_b<8>(J, bb, grid, st);
+    }
+}
+
+inline size_t minmax_head(const float *x, size_t n) {
+    size_t head = ((16 - (reinterpret_cast<uintptr_t>(x) & 15)) & 15) / 4;
+    return head > n ? n : head;
+}
+
+inline MinmaxJob minmax_job(const float *x, size_t n, float2 *partials) {
+    return MinmaxJob{x, n, minmax_head(x, n), partials, minmax_blocks(n)};
+}
+
+inline MapJob map_job(const float *x, size_t n, uint8_t *oa, float *pa, uint8_t *ob, float *pb,
+                      const float2 *partials, int np, const float *red) {
+    return MapJob{x, n, oa, ob, pa, pb, partials, np, red};
+}
+
 }  // namespace
 }  // namespace dllm
 
@@ -748,6 +964,108 @@ using namespace dllm;
 extern "C" {
 
 size_t dllm_quantize_tensor_workspace(size_t n) { return sizeof(float2) * minmax_blocks(n); }
+
+size_t dllm_quantize_kv_workspace(size_t n_k, size_t n_v) {
+    return sizeof(float2) * (minmax_blocks(n_k) + minmax_blocks(n_v));
+}
+
+int dllm_quantize_kv(const float *k, size_t n_k, const float *v, size_t n_v, uint8_t bits_a, uint8_t bits_b,
+                     int packed, uint8_t *k_a, float *kp_a, uint8_t *v_a, float *vp_a, uint8_t *k_b, float *kp_b,
+                     uint8_t *v_b, float *vp_b, void *workspace, size_t workspace_bytes, dllm_stream_t stream) {
+    if (bits_a < 1 || bits_a > 8 || bits_b > 8) return fail(DLLM_ERR_INVALID_PARAMS, "Bits must be between 1 and 8");
+    const bool two = bits_b != 0;
+    if (!kp_a || !vp_a || (two && (!kp_b || !vp_b)) || (n_k && (!k || !k_a || (two && !k_b))) ||
+        (n_v && (!v || !v_a || (two && !v_b))))
+        return fail(DLLM_ERR_INVALID_PARAMS, "null pointer");
+    const unsigned nbk = minmax_blocks(n_k), nbv = minmax_blocks(n_v);
+    if (!workspace || workspace_bytes < sizeof(float2) * (nbk + nbv))
+        return fail(DLLM_ERR_INVALID_PARAMS, "workspace too small (see dllm_quantize_kv_workspace)");
+    float2 *pk = static_cast<float2 *>(workspace), *pv = pk + nbk;
+    const bool fast = packed && n_k && n_v && fused_width(bits_a) && (!two || fused_width(bits_b)) &&
+                      aligned(k, 16) && aligned(v, 16) && aligned(k_a, 8) && aligned(v_a, 8) &&
+                      (!two || (aligned(k_b, 8) && aligned(v_b, 8))) && !fused_disabled();
+    if (!fast) {   // per tensor (same results): each quantize_tensor[_pair] uses its own partials
+        int rc = two ? dllm_quantize_tensor_pair(k, n_k, bits_a, bits_b, packed, k_a, kp_a, k_b, kp_b, pk,
+                                                 sizeof(float2) * nbk, stream)
+                     : dllm_quantize_tensor(k, n_k, bits_a, packed, k_a, kp_a, pk, sizeof(float2) * nbk, stream);
+        if (rc) return rc;
+        return two ? dllm_quantize_tensor_pair(v, n_v, bits_a, bits_b, packed, v_a, vp_a, v_b, vp_b, pv,
+                                               sizeof(float2) * nbv, stream)
+                   : dllm_quantize_tensor(v, n_v, bits_a, packed, v_a, vp_a, pv, sizeof(float2) * nbv, stream);
+    }
+    hipStream_t st = as_stream(stream);
+    int rc = launch_minmax(k, n_k, pk, nbk, st);   // min/max K
+    if (rc) return rc;
+    KVJobs J{};                                     // map K + min/max V
+    J.map[0] = map_job(k, n_k, k_a, kp_a, k_b, kp_b, pk, static_cast<int>(nbk), nullptr);
+    J.mm[0] = minmax_job(v, n_v, pv);
+    J.nmap = 1; J.nmm = 1; J.nbq = fused_grid(n_k);
+    if ((rc = launch_kv_jobs(J, bits_a, bits_b, st))) return rc;
+    KVJobs J2{};                                    // map V
+    J2.map[0] = map_job(v, n_v, v_a, vp_a, v_b, vp_b, pv, static_cast<int>(nbv), nullptr);
+    J2.nmap = 1; J2.nbq = fused_grid(n_v);
+    return launch_kv_jobs(J2, bits_a, bits_b, st);
+}
+
+int dllm_kv_extremes(const float *k, size_t n_k, const float *v, size_t n_v, float *red, void *workspace,
+                     size_t workspace_bytes, dllm_stream_t stream) {
+    if (!red || (n_k && !k) || (n_v && !v)) return fail(DLLM_ERR_INVALID_PARAMS, "null pointer");
+    if ((n_k && !aligned(k, 4)) || (n_v && !aligned(v, 4))) return fail(DLLM_ERR_INVALID_PARAMS, "x must be 4-byte aligned");
+    const unsigned nbk = minmax_blocks(n_k), nbv = minmax_blocks(n_v);
+    if (!workspace || workspace_bytes < sizeof(float2) * (nbk + nbv))
+        return fail(DLLM_ERR_INVALID_PARAMS, "workspace too small (see dllm_quantize_kv_workspace)");
+    float2 *pk = static_cast<float2 *>(workspace), *pv = pk + nbk;
+    hipStream_t st = as_stream(stream);
+    KVJobs J{};
+    if (n_k) J.mm[J.nmm++] = minmax_job(k, n_k, pk);
+    if (n_v) J.mm[J.nmm++] = minmax_job(v, n_v, pv);
+    if (J.nmm) {
+        const int rc = launch_kv_jobs(J, 1, 0, st);
+        if (rc) return rc;
+    }
+    kv_red_kernel<<<1, kBlock, 0, st>>>(pk, n_k ? static_cast<int>(nbk) : 0, pv, n_v ? static_cast<int>(nbv) : 0, red);
+    DLLM_LAUNCH_CHECK();
+    return DLLM_OK;
+}
+
+int dllm_quantize_kv_with_extremes(const float *k, size_t n_k, const float *v, size_t n_v, const float *red,
+                                   uint8_t bits_a, uint8_t bits_b, int packed, uint8_t *k_a, float *kp_a,
+                                   uint8_t *v_a, float *vp_a, uint8_t *k_b, float *kp_b, uint8_t *v_b, float *vp_b,
+                                   dllm_stream_t stream) {
+    if (bits_a < 1 || bits_a > 8 || bits_b > 8) return fail(DLLM_ERR_INVALID_PARAMS, "Bits must be between 1 and 8");
+    const bool two = bits_b != 0;
+    if (!red || !kp_a || !vp_a || (two && (!kp_b || !vp_b)) || (n_k && (!k || !k_a || (two && !k_b))) ||
+        (n_v && (!v || !v_a || (two && !v_b))))
+        return fail(DLLM_ERR_INVALID_PARAMS, "null pointer");
+    hipStream_t st = as_stream(stream);
+    const bool fast = packed && n_k && n_v && fused_width(bits_a) && (!two || fused_width(bits_b)) &&
+                      aligned(k, 16) && aligned(v, 16) && aligned(k_a, 8) && aligned(v_a, 8) &&
+                      (!two || (aligned(k_b, 8) && aligned(v_b, 8))) && !fused_disabled();
+    if (!fast) {
+        const float *rk = red, *rv = red + 2;
+        for (int t = 0; t < 2; ++t) {
+            const float *x = t ? v : k, *r = t ? rv : rk;
+            const size_t n = t ? n_v : n_k;
+            uint8_t *oa = t ? v_a : k_a, *ob = t ? v_b : k_b;
+            float *pa = t ? vp_a : kp_a, *pb = t ? vp_b : kp_b;
+            params_from_red_kernel<<<1, 64, 0, st>>>(r, bits_a, pa);
+            DLLM_LAUNCH_CHECK();
+            if (two) {
+                params_from_red_kernel<<<1, 64, 0, st>>>(r, bits_b, pb);
+                DLLM_LAUNCH_CHECK();
+            }
+            const int rc = two ? dllm_quantize_tensor_pair_with_params(x, n, bits_a, bits_b, packed, pa, pb, oa, ob, stream)
+                               : dllm_quantize_tensor_with_params(x, n, bits_a, packed, pa, oa, stream);
+            if (rc) return rc;
+        }
+        return DLLM_OK;
+    }
+    KVJobs J{};
+    J.map[0] = map_job(k, n_k, k_a, kp_a, k_b, kp_b, nullptr, 0, red);
+    J.map[1] = map_job(v, n_v, v_a, vp_a, v_b, vp_b, nullptr, 0, red + 2);
+    J.nmap = 2; J.nbq = fused_grid(std::max(n_k, n_v));
+    return launch_kv_jobs(J, bits_a, bits_b, st);
+}
 
 int dllm_quantize_tensor(const float *x, size_t n, uint8_t bits, int packed, uint8_t *out, float *params_out,
                          void *workspace, size_t workspace_bytes, dllm_stream_t stream) {

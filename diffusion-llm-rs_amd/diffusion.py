@@ -507,13 +507,13 @@ class DenoiseLoop:
         x = x.to(device=self.device, dtype=torch.float32).contiguous()
         buf = torch.empty_like(x)
         M, d = x.shape
-        main = torch.cuda.current_stream()
         if not self.overlap:
             for i, t in enumerate(range(num_steps - 1, -1, -1)):
                 self.kv_step(t, num_steps)
                 buf = self.step(x, t, i, out=buf)
                 x, buf = buf, x
             return x
+        main = torch.cuda.current_stream()
         if self._side is None:
             self._side = torch.cuda.Stream()
         if self._noise is None or self._noise[0].shape != x.shape:

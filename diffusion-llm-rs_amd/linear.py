@@ -15,6 +15,7 @@ from .quantization import _dev, _ptr, _stream
 
 
 EXACT, F16W = 0, 1   # DLLM_PRECISION_EXACT (default), DLLM_PRECISION_F16W
+PREFILL_ONLY = 0x100  # DLLM_LINEAR_PREFILL_ONLY: no decode layout (M <= 64 calls run the prefill kernels)
 
 
 class QuantLinear:
@@ -22,7 +23,9 @@ class QuantLinear:
 
     ``precision``: EXACT (default) feeds the MFMA the exact integer (q - zp) and applies the f32
     scale per group, so the weight is the reference's f32 a2 value; F16W rounds the dequantized
-    weight to f16 first (faster at M >= 4096, ~2.7e-4 more relative error per layer)."""
+    weight to f16 first (~2.7e-4 more relative error per layer, and no faster).  ``prefill_only``
+    skips the decode layout (half the device memory of an int4 layer) for layers that never see
+    M <= 64, such as every layer of the denoise loop."""
 
     def __init__(self, handle, K: int, N: int, bits: int, group: int, precision: int = EXACT):
         self._h = handle
@@ -30,24 +33,25 @@ class QuantLinear:
 
     @classmethod
     def from_weight(cls, W: torch.Tensor, bias: torch.Tensor | None = None, bits: int = 4, group: int = 128,
-                    precision: int = EXACT):
+                    precision: int = EXACT, prefill_only: bool = False):
         """W f32 [K, N] (the reference's ``weights: Array2<f32>`` of shape [input_dim, output_dim])."""
         W = _dev(W, torch.float32)
         K, N = W.shape
         b = None if bias is None else _dev(bias, torch.float32)
         h = C.c_void_p()
-        check(_lib.load().dllm_linear_create_ex(_ptr(W), _ptr(b), K, N, bits, group, int(precision), C.byref(h),
-                                                _stream()))
+        flags = int(precision) | (PREFILL_ONLY if prefill_only else 0)
+        check(_lib.load().dllm_linear_create_ex(_ptr(W), _ptr(b), K, N, bits, group, flags, C.byref(h), _stream()))
         return cls(h, K, N, bits, group, precision)
 
     @classmethod
     def from_quantized(cls, packed_codes: torch.Tensor, scales: torch.Tensor, zps: torch.Tensor, K: int, N: int,
-                       bits: int = 4, group: int = 128, bias: torch.Tensor | None = None, precision: int = EXACT):
+                       bits: int = 4, group: int = 128, bias: torch.Tensor | None = None, precision: int = EXACT,
+                       prefill_only: bool = False):
         h = C.c_void_p()
         b = None if bias is None else _dev(bias, torch.float32)
         check(_lib.load().dllm_linear_create_quantized_ex(
             _ptr(_dev(packed_codes, torch.uint8)), _ptr(_dev(scales, torch.float32)), _ptr(_dev(zps, torch.uint8)),
-            _ptr(b), K, N, bits, group, int(precision), C.byref(h), _stream()))
+            _ptr(b), K, N, bits, group, int(precision) | (PREFILL_ONLY if prefill_only else 0), C.byref(h), _stream()))
         return cls(h, K, N, bits, group, precision)
 
     def forward(self, x: torch.Tensor, out: torch.Tensor | None = None, out_dtype=torch.float16) -> torch.Tensor:
@@ -96,6 +100,14 @@ class QuantLinear:
                                                          _stream()))
         return out
 
+    @staticmethod
+    def bias_cast(y: torch.Tensor, bias: torch.Tensor | None, out_dtype=torch.float16,
+                  out: torch.Tensor | None = None) -> torch.Tensor:
+        """``y + bias`` (f32) cast to ``out_dtype`` on the device (dllm_bias_cast): the epilogue of a
+        row-parallel shard after its partial sums are reduced (parallel.RowParallelLinear)."""
+        from .quantization import bias_cast
+        return bias_cast(y, bias, out_dtype, out)
+
     def export(self):
         """-> (packed codes of the [K][N] code matrix, scales [G][N] f32, zero points [G][N] u8)."""
         G = (self.K + self.group - 1) // self.group
@@ -111,10 +123,10 @@ class QuantLinear:
         return int(_lib.load().dllm_linear_device_bytes(self._h))
 
     def set_kernel_variant(self, variant: int):
-        """Schedule variant / ablation mask: lab build only (DLLM_LIB=lab, measurement scripts)."""
+        """Schedule variant / ablation mask: lab build only (installed by `_lib.use`, measurement scripts)."""
         lib = _lib.load()
         if not hasattr(lib, "dllm_linear_set_kernel_variant"):
-            raise _lib.UnsupportedOperation("schedule variants exist only in the lab build (DLLM_LIB=lab)", 2)
+            raise _lib.UnsupportedOperation("schedule variants exist only in the lab build (_lib.use(LAB_LIB_PATH))", 2)
         check(lib.dllm_linear_set_kernel_variant(self._h, int(variant)))
 
     def weight_bytes(self) -> int:

@@ -23,12 +23,11 @@ straddle a column boundary and K/G is a whole number of groups for G <= 32.  Mod
 is not part of such a group and disables the collectives (``partial`` gives the un-reduced
 output; a row shard's ``forward`` refuses, since its output would lack the other ranks' sums and
 carry the whole bias): the one-process emulation the GPU parity tests use to compose the HIP GEMM
-with the partition logic.  ``EmulatedTensorParallel`` and ``EmulatedHeadParallelKV`` put all G
-shards of a layer / of the KV cache behind the unsharded interface, replacing each collective by
-its definition (f32 sum of the partials in rank order; max of the extremes), so that a whole
-``DenoiseLoop`` runs sharded in one process.  The local GEMM is pluggable (``local_factory``): on the GPU it is ``QuantLinear``
-(HIP kernels); the CPU multi-process tests pass the oracle's restatement so the partition and
-collective logic is checked under gloo without a GPU.
+with the partition logic (their helpers, which put all G shards behind the unsharded interface,
+live in tests/tp_emulation.py).  The local layer is pluggable (``local_factory``): on the GPU it is
+``QuantLinear`` (HIP kernels: the GEMM and the row-parallel epilogue ``bias_cast``); the CPU
+multi-process tests pass the oracle's restatement so the partition and collective logic is checked
+under gloo without a GPU.
 """
 from __future__ import annotations
 
@@ -72,8 +71,10 @@ def row_range(K: int, world: int, rank: int, group: int = 128):
 
 
 def _default_factory(W, bias, bits, group):
+    """The shards serve the denoise loop's layers (M = the tokens of a sequence): prefill-only
+    handles, without the decode layout (an M <= 64 call still runs, on the prefill kernels)."""
     from .linear import QuantLinear
-    return QuantLinear.from_weight(W, bias, bits, group)
+    return QuantLinear.from_weight(W, bias, bits, group, prefill_only=True)
 
 
 class ColumnParallelLinear:
@@ -119,16 +120,26 @@ class RowParallelLinear:
         self.k0, self.k1 = row_range(K, self.world, self.rank, group)
         self.bias = bias
         self.local = local_factory(W[self.k0:self.k1].contiguous(), None, bits, group)
+        self._pads = {}   # zero-padded f32 partial buffers of the rs_ag form, per (chunk, rows, device)
 
-    def partial(self, x: torch.Tensor, x_is_shard: bool = False) -> torch.Tensor:
-        """This rank's un-reduced f32 partial X[:, k0:k1] . W^[k0:k1, :] (no bias)."""
+    def partial(self, x: torch.Tensor, x_is_shard: bool = False, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """This rank's un-reduced f32 partial X[:, k0:k1] . W^[k0:k1, :] (no bias), into ``out`` when given."""
         xs = x if x_is_shard else x[:, self.k0:self.k1].contiguous()
-        return self.local(xs, out_dtype=torch.float32)
+        if out is None:
+            return self.local(xs, out_dtype=torch.float32)
+        return self.local(xs, out=out, out_dtype=torch.float32)
 
     def _finish(self, y: torch.Tensor, out_dtype) -> torch.Tensor:
-        if self.bias is not None:
-            y = y + self.bias.to(y.device, torch.float32)[None, :]
-        return y.to(out_dtype)
+        """The bias, once, after the reduction, and the output cast: the local layer's epilogue
+        (``QuantLinear.bias_cast`` = dllm_bias_cast, lib.rs:812)."""
+        bias = None if self.bias is None else self.bias.to(y.device, torch.float32)
+        return self.local.bias_cast(y, bias, out_dtype)
+
+    def _padded(self, c: int, Mp: int, N: int, device) -> torch.Tensor:
+        key = (c, Mp, N, str(device))
+        if key not in self._pads:   # rows past the chunk's stay zero: the GEMM writes only the first M
+            self._pads[key] = torch.zeros(Mp, N, dtype=torch.float32, device=device)
+        return self._pads[key]
 
     def forward(self, x: torch.Tensor, out_dtype=torch.float16, x_is_shard: bool = False,
                 chunks: int = 1) -> torch.Tensor:
@@ -148,14 +159,16 @@ class RowParallelLinear:
             y = self.partial(xs, True)   # partial sums stay f32 until reduced
             dist.all_reduce(y, op=dist.ReduceOp.SUM, group=self.pg)
         else:
-            parts, works = [], []
+            # each chunk's partial goes straight into its rows of y (row blocks are contiguous views)
+            y = torch.empty(xs.shape[0], self.N, dtype=torch.float32, device=xs.device)
+            works, r0 = [], 0
             for xc in torch.tensor_split(xs, min(chunks, xs.shape[0]), dim=0):
-                yc = self.partial(xc.contiguous(), True)
+                yc = y[r0:r0 + xc.shape[0]]
+                self.partial(xc, True, out=yc)
                 works.append(dist.all_reduce(yc, op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
-                parts.append(yc)
+                r0 += xc.shape[0]
             for w in works:
                 w.wait()
-            y = torch.cat(parts, dim=0)
         return self._finish(y, out_dtype)
 
     def _forward_rs_ag(self, xs: torch.Tensor, out_dtype, chunks: int) -> torch.Tensor:
@@ -165,12 +178,14 @@ class RowParallelLinear:
         split = (torch.tensor_split(xs, min(chunks, xs.shape[0]), dim=0) if chunks > 1 and xs.shape[0] > 1
                  else (xs,))
         scattered = []
-        for xc in split:
-            y = self.partial(xc.contiguous(), True)
-            M = y.shape[0]
+        for c, xc in enumerate(split):
+            M = xc.shape[0]
             Mp = -(-M // self.world) * self.world
-            if Mp != M:
-                y = torch.cat([y, y.new_zeros(Mp - M, y.shape[1])], dim=0)
+            if Mp == M:
+                y = self.partial(xc, True)
+            else:   # the chunk's rows padded to a multiple of the world with zero rows
+                y = self._padded(c, Mp, self.N, xc.device)
+                self.partial(xc, True, out=y[:M])
             mine = torch.empty(Mp // self.world, y.shape[1], dtype=torch.float32, device=y.device)
             work = dist.reduce_scatter_tensor(mine, y, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
             scattered.append((work, mine, y, M))
@@ -282,6 +297,18 @@ class DeviceKVOps:
         from .quantization import kv_attention
         return kv_attention(q, k, v)
 
+    @staticmethod
+    def kv_extremes(k, v):
+        """{-min_K, max_K, -min_V, max_V} of the local shards in one launch (dllm_kv_extremes)."""
+        from .quantization import kv_extremes
+        return kv_extremes(k, v)
+
+    @staticmethod
+    def quantize_kv(k, v, red, bits_a, bits_b):
+        """Both tensors' params and codes from the reduced extremes (dllm_quantize_kv_with_extremes)."""
+        from .quantization import quantize_kv_with_extremes
+        return quantize_kv_with_extremes(k, v, red, bits_a, bits_b, packed=True)
+
 
 class HeadParallelKVCache:
     """``QuantizedKVCacheEntry`` (diffuse-llm-rs/src/quantization.rs:140-175) with K and V sharded
@@ -304,8 +331,7 @@ class HeadParallelKVCache:
 
     def local_extremes(self, keys_local: torch.Tensor, values_local: torch.Tensor) -> torch.Tensor:
         """This rank's {-min_K, max_K, -min_V, max_V} (the all-reduce operand; NaN skipped)."""
-        sk, sv = self.ops.extremes(keys_local), self.ops.extremes(values_local)
-        return torch.stack([-sk[0], sk[1], -sv[0], sv[1]]).contiguous()
+        return _local_extremes_of(keys_local, values_local, self.ops)
 
     def quantize_with_extremes(self, keys_local: torch.Tensor, values_local: torch.Tensor, red: torch.Tensor):
         """Params and local codes from the all-reduced extremes ``red``."""
@@ -421,12 +447,20 @@ class HeadParallelKVCacheEntry(KVCacheEntry):
                                      QuantizedTensor(vc, tuple(values.shape), vp, int(bits), True), seq)
 
     def _quantize(self, keys, values, bits):
-        kp, vp = self._params(self._reduced(keys, values), bits)
+        red = self._reduced(keys, values)
+        if hasattr(self.ops, "quantize_kv"):   # both tensors' params and codes in one launch
+            (kc, kp, vc, vp), = self.ops.quantize_kv(keys, values, red, bits, 0)
+            return self._entry(keys, values, kc, kp, vc, vp, bits)
+        kp, vp = self._params(red, bits)
         return self._entry(keys, values, self.ops.quantize(keys, bits, kp), kp, self.ops.quantize(values, bits, vp),
                            vp, bits)
 
     def _quantize_pair(self, keys, values, bits_a, bits_b):
         red = self._reduced(keys, values)
+        if hasattr(self.ops, "quantize_kv"):   # both tensors at both widths in one launch
+            (kca, kpa, vca, vpa), (kcb, kpb, vcb, vpb) = self.ops.quantize_kv(keys, values, red, bits_a, bits_b)
+            return (self._entry(keys, values, kca, kpa, vca, vpa, bits_a),
+                    self._entry(keys, values, kcb, kpb, vcb, vpb, bits_b))
         (kpa, vpa), (kpb, vpb) = self._params(red, bits_a), self._params(red, bits_b)
         kca, kcb = self.ops.quantize_pair(keys, bits_a, bits_b, kpa, kpb)
         vca, vcb = self.ops.quantize_pair(values, bits_a, bits_b, vpa, vpb)
@@ -434,118 +468,8 @@ class HeadParallelKVCacheEntry(KVCacheEntry):
                 self._entry(keys, values, kcb, kpb, vcb, vpb, bits_b))
 
 
-class EmulatedHeadParallelKV:
-    """All G head shards of one KV cache entry in one process behind KVCacheEntry's interface (what
-    ``DenoiseLoop.kv_step`` calls): each quantization folds every shard's extremes, takes their max
-    (the all_reduce(MAX) by definition) and hands it to every shard.  ``keys``/``values`` are the
-    lists of shard tensors; ``get_keys``/``get_values`` concatenate the shards' hand-outs along the
-    hidden dimension (the unsharded entry's tensor, for comparison)."""
-
-    def __init__(self, keys, values, prefill_bits, decode_bits, num_heads, world, ops=DeviceKVOps):
-        hidden = keys.shape[-1]
-        self.world, self.num_heads = world, num_heads
-        self.cols = [head_columns(hidden, num_heads, world, r) for r in range(world)]
-        ks = [keys[..., c0:c1].contiguous() for c0, c1 in self.cols]
-        vs = [values[..., c0:c1].contiguous() for c0, c1 in self.cols]
-        red = torch.stack([_local_extremes_of(k, v, ops) for k, v in zip(ks, vs)]).amax(0)
-        self.shards = [HeadParallelKVCacheEntry(k, v, prefill_bits, decode_bits, ops=ops, red=red) for k, v in zip(ks, vs)]
-
-    def _reduce_for(self, keys, values):
-        red = torch.stack([s.local_extremes(k, v) for s, k, v in zip(self.shards, keys, values)]).amax(0)
-        for s in self.shards:
-            s._red_next = red
-
-    # -- KVCacheEntry's interface ------------------------------------------------------------------
-    keys = property(lambda self: [s.keys for s in self.shards])
-    values = property(lambda self: [s.values for s in self.shards])
-    is_prefill_phase = property(lambda self: self.shards[0].is_prefill_phase)
-    prefill_quant_bits = property(lambda self: self.shards[0].prefill_quant_bits)
-
-    @property
-    def decode_quant_bits(self):
-        return self.shards[0].decode_quant_bits
-
-    @decode_quant_bits.setter
-    def decode_quant_bits(self, b):
-        for s in self.shards:
-            s.decode_quant_bits = b
-
-    @property
-    def decode_quantized(self):
-        return [s.decode_quantized for s in self.shards] if self.shards[0].decode_quantized is not None else None
-
-    @decode_quantized.setter
-    def decode_quantized(self, v):
-        if v is not None:
-            raise ValueError("only None (drop the decode copy, lib.rs:900-903) can be assigned")
-        for s in self.shards:
-            s.decode_quantized = None
-
-    @property
-    def prefill_quantized(self):
-        return [s.prefill_quantized for s in self.shards] if self.shards[0].prefill_quantized is not None else None
-
-    def set_phase(self, is_prefill: bool):
-        for s in self.shards:
-            s.set_phase(is_prefill)
-
-    transition_phase = set_phase
-
-    def get_current_quant_bits(self) -> int:
-        return self.shards[0].get_current_quant_bits()
-
-    def get_keys(self):
-        return torch.cat([s.get_keys() for s in self.shards], dim=-1)
-
-    def get_values(self):
-        return torch.cat([s.get_values() for s in self.shards], dim=-1)
-
-    def update(self, new_keys, new_values):
-        """KVCacheEntry::update of every shard; ``new_keys``/``new_values`` are the shard lists (as
-        ``keys``/``values`` hand them out) or full tensors, which are split by head here."""
-        if isinstance(new_keys, torch.Tensor):
-            new_keys = [new_keys[..., c0:c1].contiguous() for c0, c1 in self.cols]
-            new_values = [new_values[..., c0:c1].contiguous() for c0, c1 in self.cols]
-        self._reduce_for(new_keys, new_values)
-        for s, k, v in zip(self.shards, new_keys, new_values):
-            s.update(k, v)
-
-    def memory_usage(self) -> int:
-        return sum(s.memory_usage() for s in self.shards)
-
-    def __len__(self):
-        return len(self.shards[0])
-
-
 def _local_extremes_of(keys, values, ops=DeviceKVOps):
+    if hasattr(ops, "kv_extremes"):
+        return ops.kv_extremes(keys, values)
     sk, sv = ops.extremes(keys), ops.extremes(values)
     return torch.stack([-sk[0], sk[1], -sv[0], sv[1]]).contiguous()
-
-
-
-class EmulatedTensorParallel:
-    """All G shards of a tensor-parallel layer (``TensorParallelPair`` or ``RowParallelLinear``
-    built with ``shard=(G, r)``) in one process behind the unsharded layer's call: the f32 partials
-    summed in rank order (the all-reduce by definition), then the bias once and the output cast --
-    what every rank holds after the pair's reduction."""
-
-    def __init__(self, shards):
-        self.shards = list(shards)
-        last = self.shards[0]
-        self.bias = (last.b if isinstance(last, TensorParallelPair) else last).bias
-
-    def __call__(self, x, out_dtype=torch.float16):
-        tot = None
-        for s in self.shards:
-            p = s.partial(x)
-            tot = p if tot is None else tot.add_(p)
-        if self.bias is not None:
-            tot = tot + self.bias.to(tot.device, torch.float32)[None, :]
-        return tot.to(out_dtype)
-
-    forward = __call__
-
-    def close(self):
-        for s in self.shards:
-            if hasattr(s, "close"):
-                s.close()

@@ -82,6 +82,86 @@ def quantize_tensor_pair(data: torch.Tensor, bits_a: int, bits_b: int, packed: b
     return (outs[0], params[0]), (outs[1], params[1])
 
 
+def _kv_outs(nk: int, nv: int, bits, packed: bool, device):
+    mk = lambda n, b: torch.empty(packed_bytes(n, b) if packed else n, dtype=torch.uint8, device=device)  # noqa: E731
+    return [(mk(nk, b), torch.empty(2, dtype=torch.float32, device=device),
+             mk(nv, b), torch.empty(2, dtype=torch.float32, device=device)) for b in bits]
+
+
+def _kv_args(outs):
+    ptr = lambda t: _ptr(t) if t.numel() else None  # noqa: E731
+    (ka, kpa, va, vpa) = outs[0]
+    b = outs[1] if len(outs) > 1 else (None, None, None, None)
+    pb = [None if t is None else (ptr(t) if t.dtype == torch.uint8 else _ptr(t)) for t in b]
+    return [ptr(ka), _ptr(kpa), ptr(va), _ptr(vpa), pb[0], pb[1], pb[2], pb[3]]
+
+
+def quantize_kv(keys: torch.Tensor, values: torch.Tensor, bits_a: int, bits_b: int = 0, packed: bool = True):
+    """QuantizedKVCacheEntry::new (quantization.rs:140-157) -- K and V each quantized per tensor --
+    at one width, or (``bits_b``) at two widths of the same K/V (KVCacheEntry::update's copies,
+    lib.rs:241-276), through dllm_quantize_kv: min/max K | map K + min/max V | map V.  Returns one
+    ``(k_codes, k_params, v_codes, v_params)`` per width, bit-identical to quantize_tensor[_pair]."""
+    bits = [int(bits_a)] + ([int(bits_b)] if bits_b else [])
+    for b in bits:
+        if not 1 <= b <= 8:
+            raise _lib.InvalidParams("Bits must be between 1 and 8")
+    k = _dev(keys, torch.float32).reshape(-1)
+    v = _dev(values, torch.float32).reshape(-1)
+    nk, nv = k.numel(), v.numel()
+    outs = _kv_outs(nk, nv, bits, packed, k.device)
+    L = _lib.load()
+    ws = torch.empty(max(L.dllm_quantize_kv_workspace(nk, nv), 16), dtype=torch.uint8, device=k.device)
+    check(L.dllm_quantize_kv(_ptr(k) if nk else None, nk, _ptr(v) if nv else None, nv, bits[0],
+                             bits[1] if len(bits) > 1 else 0, int(packed), *_kv_args(outs), _ptr(ws), ws.numel(),
+                             _stream()))
+    return outs
+
+
+def kv_extremes(keys: torch.Tensor, values: torch.Tensor) -> torch.Tensor:
+    """dllm_kv_extremes: device f32[4] {-min_K, max_K, -min_V, max_V} (NaN-ignoring fold of
+    quantization.rs:41-46) -- the operand of a head-sharded cache's one all_reduce(MAX)."""
+    k = _dev(keys, torch.float32).reshape(-1)
+    v = _dev(values, torch.float32).reshape(-1)
+    nk, nv = k.numel(), v.numel()
+    red = torch.empty(4, dtype=torch.float32, device=k.device)
+    L = _lib.load()
+    ws = torch.empty(max(L.dllm_quantize_kv_workspace(nk, nv), 16), dtype=torch.uint8, device=k.device)
+    check(L.dllm_kv_extremes(_ptr(k) if nk else None, nk, _ptr(v) if nv else None, nv, _ptr(red), _ptr(ws),
+                             ws.numel(), _stream()))
+    return red
+
+
+def quantize_kv_with_extremes(keys: torch.Tensor, values: torch.Tensor, red: torch.Tensor, bits_a: int,
+                              bits_b: int = 0, packed: bool = True):
+    """The codes and params :func:`quantize_kv` writes, with the extremes given as ``red`` =
+    {-min_K, max_K, -min_V, max_V} (already reduced over the ranks); one launch for K and V."""
+    bits = [int(bits_a)] + ([int(bits_b)] if bits_b else [])
+    for b in bits:
+        if not 1 <= b <= 8:
+            raise _lib.InvalidParams("Bits must be between 1 and 8")
+    k = _dev(keys, torch.float32).reshape(-1)
+    v = _dev(values, torch.float32).reshape(-1)
+    nk, nv = k.numel(), v.numel()
+    outs = _kv_outs(nk, nv, bits, packed, k.device)
+    check(_lib.load().dllm_quantize_kv_with_extremes(_ptr(k) if nk else None, nk, _ptr(v) if nv else None, nv,
+                                                     _ptr(_dev(red, torch.float32)), bits[0],
+                                                     bits[1] if len(bits) > 1 else 0, int(packed), *_kv_args(outs),
+                                                     _stream()))
+    return outs
+
+
+def bias_cast(y: torch.Tensor, bias: torch.Tensor | None, out_dtype=torch.float16, out: torch.Tensor | None = None):
+    """dllm_bias_cast: ``y + bias`` (f32) stored as ``out_dtype`` -- a row-parallel layer's epilogue
+    after its partial sums are reduced (diffuse-llm-rs/src/lib.rs:812)."""
+    M, N = y.shape
+    if out is None:
+        out = torch.empty(M, N, dtype=out_dtype, device=y.device)
+    dt = _lib.F16 if out.dtype == torch.float16 else _lib.F32
+    b = None if bias is None else _dev(bias, torch.float32)
+    check(_lib.load().dllm_bias_cast(_ptr(y), M, N, None if b is None else _ptr(b), _ptr(out), dt, _stream()))
+    return out
+
+
 def tensor_extremes(data: torch.Tensor, stats: torch.Tensor | None = None) -> torch.Tensor:
     """The extremes fold of quantization.rs:41-46 (NaN-ignoring) as a device f32[2] {min, max},
     folded into ``stats`` when given (seed {+inf, -inf}).  First half of :func:`quantize_tensor`
@@ -249,17 +329,17 @@ class QuantizedKVCacheEntry:
     @classmethod
     def new(cls, keys: torch.Tensor, values: torch.Tensor, bits: int, packed: bool = True):
         """quantization.rs:140-157 (keys/values are [num_layers, seq, hidden])."""
-        k = QuantizedTensor.quantize(keys, bits, packed)
-        v = QuantizedTensor.quantize(values, bits, packed)
-        return cls(k, v, int(keys.shape[1]) if keys.dim() > 1 else 0)
+        (kc, kp, vc, vp), = quantize_kv(keys, values, bits, 0, packed)
+        ks, vs = tuple(keys.shape), tuple(values.shape)
+        return cls(QuantizedTensor(kc, ks, kp, int(bits), packed), QuantizedTensor(vc, vs, vp, int(bits), packed),
+                   int(keys.shape[1]) if keys.dim() > 1 else 0)
 
     @classmethod
     def new_pair(cls, keys: torch.Tensor, values: torch.Tensor, bits_a: int, bits_b: int, packed: bool = True):
         """``new(keys, values, bits_a)`` and ``new(keys, values, bits_b)`` in one pass per tensor
         (:func:`quantize_tensor_pair`); bit-identical to the two separate calls."""
         seq = int(keys.shape[1]) if keys.dim() > 1 else 0
-        (ka, pka), (kb, pkb) = quantize_tensor_pair(keys, bits_a, bits_b, packed)
-        (va, pva), (vb, pvb) = quantize_tensor_pair(values, bits_a, bits_b, packed)
+        (ka, pka, va, pva), (kb, pkb, vb, pvb) = quantize_kv(keys, values, bits_a, bits_b, packed)
         ks, vs = tuple(keys.shape), tuple(values.shape)
         return (cls(QuantizedTensor(ka, ks, pka, int(bits_a), packed), QuantizedTensor(va, vs, pva, int(bits_a), packed), seq),
                 cls(QuantizedTensor(kb, ks, pkb, int(bits_b), packed), QuantizedTensor(vb, vs, pvb, int(bits_b), packed), seq))

@@ -100,6 +100,28 @@ int dllm_quantize_tensor_pair_with_params(const float *x, size_t n, uint8_t bits
                                           const float *params_a, const float *params_b, uint8_t *out_a,
                                           uint8_t *out_b, dllm_stream_t stream);
 
+/* ---- a3 / a8-i: both tensors of one KV-cache quantization ----------------------------------
+ * QuantizedKVCacheEntry::new(keys, values, bits) (quantization.rs:140-157: K and V each quantized
+ * per tensor by quantize_tensor) and, with bits_b != 0, KVCacheEntry::update's prefill and decode
+ * copies of the same K/V (diffuse-llm-rs/src/lib.rs:241-276): outputs bit-identical to
+ * dllm_quantize_tensor[_pair] of k and of v.  Three launches (min/max K | map K + min/max V | map V),
+ * so the map of each tensor reads it back from the Infinity Cache right after its min/max pass.
+ * bits_b = 0: one width (the *_b pointers unused).  Workspace: dllm_quantize_kv_workspace(n_k, n_v). */
+size_t dllm_quantize_kv_workspace(size_t n_k, size_t n_v);
+int dllm_quantize_kv(const float *k, size_t n_k, const float *v, size_t n_v, uint8_t bits_a, uint8_t bits_b,
+                     int packed, uint8_t *k_a, float *kp_a, uint8_t *v_a, float *vp_a, uint8_t *k_b, float *kp_b,
+                     uint8_t *v_b, float *vp_b, void *workspace, size_t workspace_bytes, dllm_stream_t stream);
+/* The same split at its reduction for a head-sharded cache: red[4] = {-min_K, max_K,
+ * -min_V, max_V} of this rank's shards (NaN-ignoring, quantization.rs:41-46; one launch over both
+ * tensors plus a fold), to be combined over the ranks by one all_reduce(MAX); then both tensors'
+ * params (:49-56) and codes (:59-65) at one or two widths in one launch.  Workspace as above. */
+int dllm_kv_extremes(const float *k, size_t n_k, const float *v, size_t n_v, float *red, void *workspace,
+                     size_t workspace_bytes, dllm_stream_t stream);
+int dllm_quantize_kv_with_extremes(const float *k, size_t n_k, const float *v, size_t n_v, const float *red,
+                                   uint8_t bits_a, uint8_t bits_b, int packed, uint8_t *k_a, float *kp_a,
+                                   uint8_t *v_a, float *vp_a, uint8_t *k_b, float *kp_b, uint8_t *v_b, float *vp_b,
+                                   dllm_stream_t stream);
+
 /* dequantize_tensor(data: &[u8], scale: f32, zero_point: f32) -> Vec<f32> (quantization.rs:81-85)
  * and QuantizedTensor::dequantize (:115-117):  y = ((q as f32) - zp) * scale.
  * params[2] = {scale, zp} in DEVICE memory (as written by dllm_quantize_tensor).
@@ -193,18 +215,25 @@ int dllm_decompress_vectors(const uint8_t *q, size_t rows, size_t dim, const flo
  *     the only operand rounding is X's (f16).  Needs group in {64, 128, 256} and K % group == 0
  *     (other shapes use the F16W arithmetic).
  *   DLLM_PRECISION_F16W: the weight is rounded to f16 (f16((q - zp) * f16(scale))) before the MFMA;
- *     ~2.7e-4 more relative error per layer, and faster at M >= 4096 (256 x 256 tiles).
+ *     ~2.7e-4 more relative error per layer (and no faster: EXACT's Horner kernel is the faster one
+ *     at M >= 4096).
  * Requirements: K % 64 == 0, group % 64 == 0; any M >= 0, any N >= 1. */
 typedef struct dllm_linear *dllm_linear_t;
 enum dllm_precision { DLLM_PRECISION_EXACT = 0, DLLM_PRECISION_F16W = 1 };
+/* Flag OR'ed into the `precision` argument of the *_create_ex calls: a prefill-only handle builds no
+ * decode layout (the 16x16x32 code image the M <= 64 kernels read): 9.02 MiB instead of 17.02 MiB at
+ * 4096 x 4096 int4 g128, the canonical codes' footprint.  Its M <= 64 calls run the prefill kernels
+ * (same precision and bound, slower at those M). */
+enum dllm_linear_flags { DLLM_LINEAR_PREFILL_ONLY = 0x100 };
 
 /* W (device, f32 [K][N] row-major), bias (device f32 [N] or NULL = zeros, the reference's
  * Array1::zeros, lib.rs:798).  Quantization runs on the GPU (bit-exact with a1).  Precision
- * DLLM_PRECISION_EXACT.  Create builds everything a forward reads -- the prefill and decode code
- * layouts, the per-(group, column) parameters and, for int4 g128 EXACT handles with N % 256 == 0,
- * the Horner-form ratios s_{g-1}/s_g with the check that the scales allow that form -- in
- * temporaries of its own, and synchronises `stream` once before it returns (it is not capturable).
- * The handle is immutable afterwards: safe to share across threads on distinct streams. */
+ * DLLM_PRECISION_EXACT.  Create builds everything a forward reads -- the prefill and (unless
+ * DLLM_LINEAR_PREFILL_ONLY) decode code layouts, the per-(group, column) parameters and, for int4
+ * g128 EXACT handles with N % 256 == 0, the Horner-form ratios s_{g-1}/s_g with the check that the
+ * scales allow that form -- in temporaries of its own, and synchronises `stream` once before it
+ * returns (it is not capturable).  The handle is immutable afterwards and its forwards keep their
+ * scratch per (device, stream): one handle may serve several threads on distinct streams. */
 int dllm_linear_create(const float *W, const float *bias, size_t K, size_t N, uint8_t bits, size_t group,
                        dllm_linear_t *out, dllm_stream_t stream);
 int dllm_linear_create_ex(const float *W, const float *bias, size_t K, size_t N, uint8_t bits, size_t group,
@@ -218,7 +247,7 @@ int dllm_linear_create_quantized_ex(const uint8_t *packed_codes, const float *sc
                                     const float *bias, size_t K, size_t N, uint8_t bits, size_t group,
                                     int precision, dllm_linear_t *out, dllm_stream_t stream);
 /* Y[M][N] = X[M][K] . W^ + b.  x_dtype/y_dtype in {DLLM_F32, DLLM_F16}; an f32 X is cast to f16
- * through a workspace owned by the handle.  Shapes with too few output tiles to fill the GPU
+ * through a per-(device, stream) staging workspace.  Shapes with too few output tiles to fill the GPU
  * (M roughly 65..1000 at N = 4096) split K into slices whose f32 partials are combined in slice
  * order (deterministic) through a per-(device, stream) workspace.  Both workspaces only grow and
  * are allocated on the first call that needs them, which therefore must precede stream capture.
@@ -229,6 +258,13 @@ int dllm_linear_create_quantized_ex(const uint8_t *packed_codes, const float *sc
  * (same bound, different f32 summation order). */
 int dllm_linear_forward(dllm_linear_t h, const void *X, size_t M, int x_dtype, void *Y, int y_dtype,
                         dllm_stream_t stream);
+/* The epilogue of a row-parallel layer after its partial sums are reduced over the ranks
+ * (parallel.RowParallelLinear): out[m][n] = y[m][n] + bias[n] in f32 -- the
+ * reference's `x.dot(&self.weights) + &self.bias` (diffuse-llm-rs/src/lib.rs:812), the bias added
+ * once after the reduction -- stored as f32 (out may equal y) or RNE f16.  bias NULL = zeros.
+ * y, out [M][N] device; asynchronous on `stream`. */
+int dllm_bias_cast(const float *y, size_t M, size_t N, const float *bias, void *out, int out_dtype,
+                   dllm_stream_t stream);
 /* Export the quantized weights in canonical form (packed bitstream [K][N], scales [G][N], zps);
  * the codes are rebuilt from the device layout (the handle keeps no canonical copy). */
 int dllm_linear_export(dllm_linear_t h, uint8_t *packed_codes, float *scales, uint8_t *zps,
@@ -238,8 +274,8 @@ int dllm_linear_precision(dllm_linear_t h);   /* DLLM_PRECISION_*, -1 on a null 
 /* HBM bytes the forward's GEMM kernel reads for the weights (packed codes + scales/zps). */
 size_t dllm_linear_weight_bytes(dllm_linear_t h);
 /* Device memory the handle owns: the prefill and decode code layouts and the per-(group, column)
- * parameters (f16 zero-point/scale pairs + f32 scales) -- 17.02 MiB at 4096 x 4096 int4 g128 --
- * plus the Horner ratios where kept (+0.52 MiB there) and the X staging workspace once grown. */
+ * parameters (f16 zero-point/scale pairs + f32 scales) -- 17.02 MiB at 4096 x 4096 int4 g128, 9.02
+ * MiB prefill-only -- plus the Horner ratios where kept (+0.52 MiB there). */
 size_t dllm_linear_device_bytes(dllm_linear_t h);
 #ifdef DLLM_LAB
 /* Lab build only (libdllm_hip_lab.so): A/B schedule variants and ablation masks; mutates the

@@ -8,7 +8,7 @@ CODE = r"""
 import sys, json, torch
 sys.path.insert(0, %r)
 import __graft_entry__ as g
-d = g.load_package()
+d = g.load_package(); import scripts._lab as _lab; _lab.select(d)
 S, H, D = 8192, 32, 128
 torch.manual_seed(0)
 K = torch.randn(S, H, D, device='cuda'); V = torch.randn(S, H, D, device='cuda'); Q = torch.randn(S, H, D, device='cuda').half()

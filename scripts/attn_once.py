@@ -5,7 +5,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 import torch
 import __graft_entry__ as g
 
-d = g.load_package()
+d = g.load_package(); import scripts._lab as _lab; _lab.select(d)
 S, H, D = [int(a) for a in sys.argv[1:4]] if len(sys.argv) > 3 else (8192, 32, 128)
 K = torch.randn(S, H, D, device="cuda"); V = torch.randn(S, H, D, device="cuda")
 Q = torch.randn(S, H, D, device="cuda").half()

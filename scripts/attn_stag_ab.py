@@ -14,7 +14,7 @@ sys.path.insert(0, str(ROOT))
 import torch
 import __graft_entry__ as g
 
-d = g.load_package(); d.load_library()
+d = g.load_package(); import scripts._lab as _lab; _lab.select(d)
 labs = [int(v) for v in (sys.argv[1:] or ["0", "302", "198"])]
 
 

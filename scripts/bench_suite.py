@@ -22,7 +22,7 @@ import torch
 
 import __graft_entry__ as g
 
-d = g.load_package()
+d = g.load_package(); import scripts._lab as _lab; _lab.select(d)
 dev = torch.device("cuda")
 HBM = 8.0e12
 PEAK = 2.5e15

@@ -11,7 +11,7 @@ import torch
 
 import __graft_entry__ as g
 
-d = g.load_package()
+d = g.load_package(); import scripts._lab as _lab; _lab.select(d)
 dev = torch.device("cuda")
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 50
 want = sys.argv[2].split(",") if len(sys.argv) > 2 else ["product", "product_cast", "serial", "nokv"]

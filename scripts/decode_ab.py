@@ -12,7 +12,7 @@ sys.path.insert(0, str(ROOT))
 import torch
 import __graft_entry__ as g
 
-d = g.load_package(); d.load_library()
+d = g.load_package(); import scripts._lab as _lab; _lab.select(d)
 var = int(sys.argv[1])
 Ms = [int(m) for m in (sys.argv[2:] or ["1", "16", "32", "64"])]
 K = N = 4096

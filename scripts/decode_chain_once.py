@@ -9,7 +9,7 @@ import torch
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 import __graft_entry__ as g  # noqa: E402
 
-d = g.load_package()
+d = g.load_package(); import scripts._lab as _lab; _lab.select(d)
 M = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 K = N = 4096
 L = 40

@@ -13,7 +13,7 @@ CODE = r"""
 import sys, json, time, torch
 sys.path.insert(0, %r)
 import __graft_entry__ as g
-d = g.load_package()
+d = g.load_package(); import scripts._lab as _lab; _lab.select(d)
 K = N = 4096
 L = 40
 gen = torch.Generator(device="cuda").manual_seed(7)

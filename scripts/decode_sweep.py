@@ -13,7 +13,7 @@ import torch
 
 import __graft_entry__ as g
 
-d = g.load_package()
+d = g.load_package(); import scripts._lab as _lab; _lab.select(d)
 dev = torch.device("cuda")
 K = N = int(os.environ.get("DIM", "4096"))
 L = int(os.environ.get("LAYERS", "48"))

@@ -12,7 +12,7 @@ CODE = r"""
 import sys, json, time, torch
 sys.path.insert(0, %r)
 import __graft_entry__ as g
-d = g.load_package()
+d = g.load_package(); import scripts._lab as _lab; _lab.select(d)
 n = 8192 * 4096
 x = torch.randn(n, device="cuda")
 q, params = d.quantize_tensor(x, 4, packed=True)

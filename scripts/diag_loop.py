@@ -5,15 +5,16 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 import torch
 import __graft_entry__ as g
+from tests import tp_emulation as emu
 
-dllm = g.load_package(); dllm.load_library()
+dllm = g.load_package(); import scripts._lab as _lab; _lab.select(dllm)
 par = dllm.parallel
 d, M, L, steps, seed, G = 4096, 2048, 12, 50, 7, 2
 gen = torch.Generator(device="cuda").manual_seed(7)
 Ws = [(1.0 / 64.0) * torch.randn(d, d, device="cuda", generator=gen) for _ in range(L)]
 x = torch.randn(M, d, device="cuda", generator=gen)
 unsh = [dllm.QuantLinear.from_weight(W, None, 4, 128) for W in Ws]
-pairs = [par.EmulatedTensorParallel([par.TensorParallelPair(Ws[2 * p], None, Ws[2 * p + 1], None, 4, 128,
+pairs = [emu.EmulatedTensorParallel([par.TensorParallelPair(Ws[2 * p], None, Ws[2 * p + 1], None, 4, 128,
                                                             shard=(G, r)) for r in range(G)]) for p in range(L // 2)]
 rel = lambda a, b: ((a.double() - b.double()).norm() / b.double().norm()).item()
 hu, hs = x, x

@@ -6,9 +6,10 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 import torch
 import __graft_entry__ as g
+from tests import tp_emulation as emu
 from oracle import oracle as orc
 
-d = g.load_package(); d.load_library()
+d = g.load_package(); import scripts._lab as _lab; _lab.select(d)
 par = d.parallel
 D, M, G = 4096, 2048, 2
 gen = torch.Generator(device="cuda").manual_seed(7)
@@ -39,7 +40,7 @@ pairs = [par.TensorParallelPair(WA, None, WB, None, 4, 128, shard=(G, r)) for r 
 hs = torch.cat([p.a(x, out_dtype=torch.float16) for p in pairs], dim=1)
 print("A column shards f16 == unsharded:", torch.equal(hs, h_u), "rel", rel(hs.float(), h_u.float()),
       "differing elems", (hs != h_u).sum().item())
-em = par.EmulatedTensorParallel(pairs)
+em = emu.EmulatedTensorParallel(pairs)
 y_s = em(x, out_dtype=torch.float32)
 print("pair sharded vs unsharded f32:", rel(y_s, y_u))
 print("pair sharded vs f64:", rel(y_s, y_64))

@@ -12,7 +12,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 import torch
 import __graft_entry__ as g
 
-d = g.load_package()
+d = g.load_package(); import scripts._lab as _lab; _lab.select(d)
 shapes = [tuple(int(v) for v in a.split(":")) for a in sys.argv[1:]] or [(2048, 4096), (4096, 4096), (4096, 2048),
                                                                          (4096, 1024), (4096, 512), (1024, 4096),
                                                                          (256, 4096)]

@@ -9,7 +9,7 @@ CODE = r"""
 import sys, json, torch
 sys.path.insert(0, %r)
 import __graft_entry__ as g
-d = g.load_package()
+d = g.load_package(); import scripts._lab as _lab; _lab.select(d)
 K = 4096
 out = {}
 for sh in %r.split(","):

@@ -10,7 +10,7 @@ sys.path.insert(0, str(ROOT))
 import torch
 import __graft_entry__ as g
 
-d = g.load_package(); d.load_library()
+d = g.load_package(); import scripts._lab as _lab; _lab.select(d)
 M = N = 4096
 res = []
 for K in [int(a) for a in (sys.argv[1:] or ["128", "256", "512", "1024", "2048", "4096"])]:

@@ -6,7 +6,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 import torch
 import __graft_entry__ as g
 
-d = g.load_package()
+d = g.load_package(); import scripts._lab as _lab; _lab.select(d)
 Ms = [int(a) for a in sys.argv[1:]] or [2048, 4096]
 VARS = [int(v) for v in __import__("os").environ.get("VARS", "0,1,2,3").split(",")]
 K = N = 4096

@@ -13,7 +13,7 @@ sys.path.insert(0, str(ROOT))
 import torch
 import __graft_entry__ as g
 
-d = g.load_package(); d.load_library()
+d = g.load_package(); import scripts._lab as _lab; _lab.select(d)
 M = N = K = int(os.environ.get("AB_K", "4096"))
 M = int(os.environ.get("AB_M", str(M)))
 W = 0.02 * torch.randn(K, N, device="cuda")

@@ -10,7 +10,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 import torch
 import __graft_entry__ as g
 
-d = g.load_package()
+d = g.load_package(); import scripts._lab as _lab; _lab.select(d)
 x = torch.randn(1 << 28, device="cuda")          # 1 GiB, larger than the 256 MiB Infinity Cache
 flush = torch.empty(1 << 28, device="cuda")
 for _ in range(5):

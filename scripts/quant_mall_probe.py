@@ -14,7 +14,7 @@ import torch
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 import __graft_entry__ as g  # noqa: E402
 
-d = g.load_package()
+d = g.load_package(); import scripts._lab as _lab; _lab.select(d)
 from dllm_amd import quantization as dq  # noqa: E402
 n = 8192 * 4096
 x = torch.randn(n, device="cuda")

@@ -8,7 +8,7 @@ import torch
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 import __graft_entry__ as g  # noqa: E402
 
-dllm = g.load_package()
+dllm = g.load_package(); import scripts._lab as _lab; _lab.select(dllm)
 n_iter = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 x = torch.randn(8192 * 4096, device="cuda")
 k = torch.randn(8192 * 4096, device="cuda")

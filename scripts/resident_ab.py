@@ -7,7 +7,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 import torch
 import __graft_entry__ as g
 
-d = g.load_package()
+d = g.load_package(); import scripts._lab as _lab; _lab.select(d)
 n = 8192 * 4096
 x = torch.randn(n, device="cuda")
 cases = {"int4": lambda: d.quantize_tensor(x, 4, packed=True),

@@ -10,7 +10,7 @@ import __graft_entry__ as g
 
 WARM, REPS = 5, 20
 Ms = [int(a) for a in sys.argv[1:]] or [1, 4, 16, 32, 64, 128, 256, 512, 1024, 2048, 4096, 8192]
-d = g.load_package()
+d = g.load_package(); import scripts._lab as _lab; _lab.select(d)
 K = N = 4096
 torch.manual_seed(0)
 W = 0.02 * torch.randn(K, N, device="cuda")

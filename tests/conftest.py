@@ -42,6 +42,8 @@ def dllm():
     """The product package (HIP path).  Fails loudly if the library is missing."""
     import __graft_entry__ as g
     mod = g.load_package()
+    from scripts import _lab   # DLLM_LIB=lab: the lab tests install the lab build explicitly
+    _lab.select(mod)
     mod.load_library()
     return mod
 

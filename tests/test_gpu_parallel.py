@@ -18,6 +18,8 @@ policy, so every shard shape runs through the HIP kernels it will use on G GPUs.
 import numpy as np
 import pytest
 
+from tests import tp_emulation as emu
+
 pytestmark = pytest.mark.gpu
 
 REL_TOL = 1e-3
@@ -164,8 +166,8 @@ def test_denoise_loop_config5_sharded(dllm, torch, orc, G):
     853-955): 12 int4 g128 layers of d 4096 as 6 hidden-dim-sharded Megatron pairs, seq 2048, 50
     steps, with the phase-aware KV cache (8 / 4 bits, progressive precision on, lib.rs:121-313,
     884-918) sharded by head (32 heads of 128) -- G ranks emulated in one process
-    (parallel.EmulatedTensorParallel: the pair's f32 partials summed in rank order;
-    parallel.EmulatedHeadParallelKV: one max of the shards' K/V extremes per quantization), against
+    (tp_emulation.EmulatedTensorParallel: the pair's f32 partials summed in rank order;
+    tp_emulation.EmulatedHeadParallelKV: one max of the shards' K/V extremes per quantization), against
     the unsharded loop (QuantLinear layers, KVCacheEntry) and the f32 chain.  Teacher-forced: every
     step maps the sharded run's own x_t through (a) the sharded step, (b) the unsharded step, (c) the
     reference in f32 (x.dot(W) per layer on the oracle-dequantized weights, lib.rs:806-813, then
@@ -192,11 +194,11 @@ def test_denoise_loop_config5_sharded(dllm, torch, orc, G):
     x = torch.randn(M, d, device="cuda", generator=g)
     unsh = [dllm.QuantLinear.from_weight(W, None, 4, 128) for W in Ws]
     Wh = [_dequantized(lin, orc) for lin in unsh]
-    pairs = [par.EmulatedTensorParallel([par.TensorParallelPair(Ws[2 * p], None, Ws[2 * p + 1], None, 4, 128,
+    pairs = [emu.EmulatedTensorParallel([par.TensorParallelPair(Ws[2 * p], None, Ws[2 * p + 1], None, 4, 128,
                                                                 shard=(G, r)) for r in range(G)])
              for p in range(L // 2)]
     kv_u = dllm.KVCacheEntry.new(K, V, cfg.prefill_bits, cfg.decode_bits)
-    kv_s = par.EmulatedHeadParallelKV(K, V, cfg.prefill_bits, cfg.decode_bits, heads, G)
+    kv_s = emu.EmulatedHeadParallelKV(K, V, cfg.prefill_bits, cfg.decode_bits, heads, G)
     loop_u = dllm.DenoiseLoop(unsh, cfg, cumprod=dllm.Cumprod.INCLUSIVE, seed=seed, kv_cache=kv_u, overlap=False)
     loop_s = dllm.DenoiseLoop(pairs, cfg, cumprod=dllm.Cumprod.INCLUSIVE, seed=seed, kv_cache=kv_s, overlap=False)
     errs, errs_u, widths = [], [], []

@@ -448,7 +448,7 @@ def test_linear_split_k_exact_integers(dllm, torch, orc):
 @pytest.mark.parametrize("precision", [0, 1])
 @pytest.mark.parametrize("bits", [2, 4, 8])
 @pytest.mark.parametrize("M,N", [(4096, 4096), (2048, 4096), (1800, 4096), (4096, 1024), (4096, 512), (512, 1024),
-                                 (300, 256), (64, 200), (33, 200), (17, 200), (1, 200)])
+                                 (300, 256), (64, 200), (33, 200), (17, 200), (1, 200), (4096, 4092), (2048, 4092)])
 def test_linear_policy_exact_integers(dllm, torch, orc, precision, bits, M, N):
     """Every tile of both precision policies on exact-integer data (each group spans [0, 2^b - 1]:
     scale 1, zp 0; K = 768 = 6 groups, so every product and partial sum is an exact integer):
@@ -456,7 +456,9 @@ def test_linear_policy_exact_integers(dllm, torch, orc, precision, bits, M, N):
     128 x 128 + group-aligned split-K
     (N 1024 / 512, M 512, 300), the exact decode kernel (M <= 64, one or 4 column tiles, K split) --
     and rounded weights (256 x 256, 256 x 128 two k-groups, 128 x 128 split-K, decode), with bias,
-    ragged M and a padded last column group: bit-equal to the f64 product, f32 and f16 outputs."""
+    ragged M and a padded last column group: bit-equal to the f64 product, f32 and f16 outputs.
+    N = 4092 (N % 8 == 4: every other output row starts 8-B aligned) takes the Horner grid (M 4096)
+    and the 128 x 256 exact tiles (M 2048) on their 8-B row-store path, not the 16-B coalesced one."""
     K = 768
     rng = np.random.default_rng(100 * bits + M + N + precision)
     q = (1 << bits) - 1
@@ -958,3 +960,98 @@ def test_head_parallel_kv_cache_bitexact(dllm, torch, orc, S, H, G, bits):
         e = kv.entry(loc[1], loc[2], red)
         O = kv.attention(loc[0], e)
         assert torch.equal(O, O_full[:, kv.h0:kv.h1]), "per-head attention must not depend on the shard"
+
+
+def test_linear_prefill_only_handle(dllm, torch, orc):
+    """DLLM_LINEAR_PREFILL_ONLY: no decode layout -- 8 MiB of codes + 1 MiB of sz/sf parameters +
+    the bias (9.02 MiB, the canonical footprint) plus the 0.52 MiB of Horner ratios at 4096^2 int4
+    g128, against 17.54 MiB for the full handle -- and its M <= 64 calls run the prefill kernels:
+    within the exact-weight bound of the f32 product on the same f16 X, like the decode kernels of
+    the full handle; M > 64 calls are the same kernels as the full handle's, bit for bit."""
+    K = N = 4096
+    W = 0.02 * torch.randn(K, N, device="cuda")
+    full = dllm.QuantLinear.from_weight(W, None, 4, 128)
+    pre = dllm.QuantLinear.from_weight(W, None, 4, 128, prefill_only=True)
+    assert full.device_bytes() - pre.device_bytes() == K * N // 2          # exactly the decode layout
+    assert pre.device_bytes() == K * N // 2 + 32 * N * 8 + N * 4 + 33 * N * 4, pre.device_bytes()
+    codes, scales, zps = full.export()
+    c2, s2, z2 = pre.export()
+    assert torch.equal(codes, c2) and torch.equal(scales, s2) and torch.equal(zps, z2)
+    cw, cs, cz = (host(t) for t in (codes, scales, zps))
+    Wh = orc.dequantize_weights(orc.unpack_bits(cw, K * N, 4).reshape(K, N), cs, cz, 128)
+    Wt = torch.from_numpy(Wh).cuda()
+    for M in (1, 17, 64, 65, 300, 2048):
+        X = torch.randn(M, K, device="cuda").half()
+        ref = X.float() @ Wt
+        y = pre(X, out_dtype=torch.float32)
+        rel = float((y - ref).norm() / ref.norm())
+        assert rel <= 2e-5, (M, rel)
+        if M > 64:
+            assert torch.equal(y, full(X, out_dtype=torch.float32)), M
+    full.close()
+    pre.close()
+
+
+def test_bias_cast(dllm, torch):
+    """dllm_bias_cast (the row-parallel epilogue): y + bias in f32, then RNE f16 or f32; vector and
+    scalar paths (N % 4), no bias, f32 in place."""
+    for M, N in ((2048, 4096), (33, 1027), (5, 3)):
+        y = torch.randn(M, N, device="cuda")
+        b = torch.randn(N, device="cuda")
+        ref = y + b[None, :]
+        assert torch.equal(dllm.quantization.bias_cast(y, b, torch.float16), ref.half())
+        assert torch.equal(dllm.quantization.bias_cast(y, b, torch.float32), ref)
+        assert torch.equal(dllm.quantization.bias_cast(y, None, torch.float16), y.half())
+        yy = y.clone()
+        dllm.quantization.bias_cast(yy, b, torch.float32, out=yy)
+        assert torch.equal(yy, ref)
+
+
+@pytest.mark.parametrize("nk,nv", [(1, 1), (7, 9), (2047, 2048), (2048, 2049), (100003, 77777), (1 << 21, 1 << 21),
+                                   (8192 * 32 * 128, 8192 * 32 * 128)])
+@pytest.mark.parametrize("bits_a,bits_b", [(4, 0), (8, 4), (2, 1), (1, 8)])
+def test_quantize_kv_matches_per_tensor(dllm, torch, orc, nk, nv, bits_a, bits_b):
+    """dllm_quantize_kv (min/max K | map K + min/max V | map V, the coalesced map) against
+    dllm_quantize_tensor[_pair] of each tensor: codes and params bit-identical at one and two widths,
+    ragged sizes (partial chunks and tail octets); and the split form (dllm_kv_extremes +
+    dllm_quantize_kv_with_extremes) likewise.  The smaller sizes are also checked against the oracle."""
+    if nk > (1 << 21) and (bits_a, bits_b) not in ((4, 0), (8, 4)):
+        pytest.skip("full C4 size at the KV cache's widths only")
+    q = dllm.quantization
+    g = torch.Generator(device="cuda").manual_seed(nk + 3 * nv + bits_a)
+    k = torch.randn(nk, device="cuda", generator=g) * 2 + 0.25
+    v = torch.randn(nv, device="cuda", generator=g) * 0.5 - 1
+    outs = q.quantize_kv(k, v, bits_a, bits_b)
+    for w, bits in enumerate([bits_a] + ([bits_b] if bits_b else [])):
+        kc, kp, vc, vp = outs[w]
+        for x, c, pr in ((k, kc, kp), (v, vc, vp)):
+            rc, rp = q.quantize_tensor(x, bits, packed=True)
+            assert torch.equal(c, rc) and same_bits(host(pr), host(rp)), (w, bits)
+    red = q.kv_extremes(k, v)
+    ek, ev = q.tensor_extremes(k), q.tensor_extremes(v)
+    assert same_bits(host(red), host(torch.stack([-ek[0], ek[1], -ev[0], ev[1]])))
+    outs2 = q.quantize_kv_with_extremes(k, v, red, bits_a, bits_b)
+    for a, b in zip(outs, outs2):
+        for ta, tb in zip(a, b):
+            assert torch.equal(ta, tb)
+    if nk <= 100003:
+        rq, rs, rz = orc.quantize_tensor(host(k), bits_a)
+        assert np.array_equal(host(outs[0][0]), orc.pack_bits(rq, bits_a))
+        assert host(outs[0][1]).tobytes() == np.array([rs, rz], np.float32).tobytes()
+
+
+def test_quantize_kv_unaligned_and_empty(dllm, torch):
+    """The generic fallbacks of dllm_quantize_kv: a K/V base not 16-B aligned, unpacked codes and an
+    empty tensor give what quantize_tensor gives."""
+    q = dllm.quantization
+    base = torch.randn(70001, device="cuda")
+    k, v = base[1:50001], base[50001:]
+    for packed in (True, False):
+        (kc, kp, vc, vp), = q.quantize_kv(k, v, 4, 0, packed)
+        rk, rkp = q.quantize_tensor(k, 4, packed=packed)
+        rv, rvp = q.quantize_tensor(v, 4, packed=packed)
+        assert torch.equal(kc, rk) and torch.equal(vc, rv) and same_bits(host(kp), host(rkp)) and same_bits(host(vp), host(rvp))
+    e = torch.empty(0, device="cuda")
+    (kc, kp, vc, vp), = q.quantize_kv(e, v, 4, 0)
+    rk, rkp = q.quantize_tensor(e, 4, packed=True)
+    assert kc.numel() == 0 and same_bits(host(kp), host(rkp))

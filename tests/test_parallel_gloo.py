@@ -27,12 +27,25 @@ class OracleLinear:
         self.What = orc.dequantize_weights(self.codes, self.scales, self.zps, group)
         self.bias = None if bias is None else bias.detach().cpu().numpy().astype(np.float32)
 
-    def __call__(self, x, out_dtype=torch.float32):
+    def __call__(self, x, out_dtype=torch.float32, out=None):
         X = x.detach().cpu().numpy().astype(np.float32)
         Y = (X.astype(np.float64) @ self.What.astype(np.float64))
         if self.bias is not None:
             Y = Y + self.bias[None, :]
-        return torch.from_numpy(Y.astype(np.float32)).to(out_dtype)
+        y = torch.from_numpy(Y.astype(np.float32)).to(out_dtype)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+
+    @staticmethod
+    def bias_cast(y, bias, out_dtype=torch.float16, out=None):
+        """The row-parallel epilogue (bias after the reduction, then the cast), in f32 on the CPU."""
+        r = (y if bias is None else y + bias.to(torch.float32)[None, :]).to(out_dtype)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
 
 
 def _free_port():
