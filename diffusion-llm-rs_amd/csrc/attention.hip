@@ -1003,8 +1003,8 @@ extern "C" int dllm_kv_attention(const void *Q, const uint8_t *Kq, const float *
     if (S * H * D * bits / 8 >= (size_t{1} << 31) || H > 65535)
         return fail(DLLM_ERR_SHAPE_MISMATCH, "K/V codes must stay below 2 GiB (32-bit buffer offsets)");
     if ((reinterpret_cast<uintptr_t>(Kq) & 15) || (reinterpret_cast<uintptr_t>(Vq) & 15) ||
-        (reinterpret_cast<uintptr_t>(Q) & 15))
-        return fail(DLLM_ERR_INVALID_PARAMS, "Q, K and V codes must be 16-byte aligned");
+        (reinterpret_cast<uintptr_t>(Q) & 15) || (reinterpret_cast<uintptr_t>(O) & 15))
+        return fail(DLLM_ERR_INVALID_PARAMS, "Q, O, K and V codes must be 16-byte aligned");   // O: 16-B row stores
     hipStream_t st = as_stream(stream);
     const int nkb = static_cast<int>((S + kKB - 1) / kKB);
     uint8_t *img = reinterpret_cast<uint8_t *>(device_workspace(st, static_cast<size_t>(H) * nkb * kImg, 8));

@@ -1,6 +1,7 @@
 // capi.cpp -- library-level C-ABI entry points (errors, version, device probe).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -45,6 +46,36 @@ float *device_workspace(hipStream_t st, size_t bytes, int slot) {
         return nullptr;
     }
     e = {p, bytes};
+    return p;
+}
+
+unsigned *zeroed_counters(hipStream_t st, size_t n) {
+    static std::mutex mu;
+    static std::map<std::pair<int, hipStream_t>, std::pair<unsigned *, size_t>> pool;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(mu);
+    auto &e = pool[{dev, st}];
+    if (e.second >= n) return e.first;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(st, &cs);
+    if (cs != hipStreamCaptureStatusNone) {
+        fail(DLLM_ERR_HIP, "hand-off words must be allocated before stream capture (run the shape once first)");
+        return nullptr;
+    }
+    if (e.first) {
+        if (hipStreamSynchronize(st) != hipSuccess) return nullptr;
+        (void)hipFree(e.first);
+        e = {nullptr, 0};
+    }
+    unsigned *p = nullptr;
+    const size_t cap = std::max<size_t>(n, 64);
+    if (hipMalloc(reinterpret_cast<void **>(&p), cap * sizeof(unsigned)) != hipSuccess ||
+        hipMemsetAsync(p, 0, cap * sizeof(unsigned), st) != hipSuccess) {
+        fail(DLLM_ERR_HIP, "hipMalloc of the hand-off words failed");
+        return nullptr;
+    }
+    e = {p, cap};
     return p;
 }
 

@@ -44,6 +44,9 @@ inline hipStream_t as_stream(dllm_stream_t s) { return reinterpret_cast<hipStrea
 // may still use the old buffer) and is refused while the stream is being captured.  Returns null
 // (error set) on failure.
 float *device_workspace(hipStream_t st, size_t bytes, int slot = 0);
+// Grow-only per-(device, stream) array of u32 words, zeroed when (re)allocated (outside stream
+// capture): the grid hand-off words of quant_resident.hip, whose kernels leave them reusable.
+unsigned *zeroed_counters(hipStream_t st, size_t n);
 
 typedef __attribute__((address_space(3))) void *lds_void_ptr;
 typedef __attribute__((address_space(1))) void *gbl_void_ptr;

@@ -74,13 +74,15 @@ __device__ __forceinline__ void horner_burst(__amdgpu_buffer_rsrc_t xr, uint32_t
 // MODE bit 0: the staggered schedule (product).  Lab ablations only (results wrong, timing only):
 // bit 1 no output stores; bit 2 no Horner rescale; bit 3 one dequant per k-step instead of four;
 // bit 4 one B fragment read per k-step instead of four; bit 5 no X DMA (weight words only); bit 6
-// no DMA at all.
+// no DMA at all; bit 7 no MFMA (the DMA ring, waits and barriers alone).  Bit 8 (product): the
+// stage's DMA pieces spread one per MFMA pair over the second half k-step instead of one burst
+// (bit-identical; 124.9 -> 123.6 us at M = 4096 in one process, profiles/r04_horner/).
 template <typename YT, int EPI, int MODE>
 __global__ void __launch_bounds__(512, 1)
 wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdev,
                  const uint32_t *__restrict__ sz, const float *__restrict__ hr, const float *__restrict__ sf,
                  const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad, int nbm, int nbn,
-                 PSampleEpi epi) {
+                 PSampleEpi epi, int grows = 0) {
     constexpr bool STAG = MODE & 1;
     __shared__ __attribute__((aligned(16))) uint8_t smem[3 * kHStage];
 
@@ -89,7 +91,14 @@ wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
     const int nb = nbm * nbn, orig = blockIdx.x;
     const int xcd = orig % kXCDs, q8 = nb / kXCDs, r8 = nb % kXCDs;
     const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / kXCDs;
-    const int bm = tile / nbn, bn = tile % nbn;
+    int bm = tile / nbn, bn = tile % nbn;
+    if (DLLM_LAB && (grows == 2 || grows == 4 || grows == 8 || grows == 16) && nb == 256 && nbm == 16 && nbn == 16) {
+        // lab A/B: each XCD's 32 tiles as grows row-blocks x (32 / grows) column-blocks (grows in
+        // {2, 4, 8, 16}: 32 / grows must tile the 16 column blocks; every bm, bn stays in 0..15)
+        const int gc = 32 / grows, reg = tile / 32, loc = tile % 32, per_row = 16 / gc;
+        bm = (reg / per_row) * grows + loc / gc;
+        bn = (reg % per_row) * gc + loc % gc;
+    }
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int m0 = bm * 256, n0 = bn * 256;
@@ -151,10 +160,57 @@ wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
     uint32_t w[4];
     float4 r4[4];
     half8_t bA[8], bB[8], aA, aB;
+    // MODE bit 8: the pending stage's pieces, issued between MFMA pairs of substeps 2 and 3
+    int pend_slot = 0, pend_kt = 0;
+    bool pend_gf = false, pend_on = false;
+    auto piece = [&](int p) __attribute__((always_inline)) {
+        if (!pend_on) return;
+        const uint32_t base = sbase + static_cast<uint32_t>(pend_slot * kHStage);
+        if (p < 4)
+            blds16_asm(xr, xo[p], static_cast<uint32_t>(pend_kt * kBK * 2),
+                       base + static_cast<uint32_t>(wave * 1024 + p * 0x2000));
+        else if (p == 4)
+            blds16_asm(wr, wo, static_cast<uint32_t>(pend_kt * 1024), base + static_cast<uint32_t>(kHX + wave * 1024));
+        else if (pend_gf && has_g)
+            blds16_asm(gr, wo, static_cast<uint32_t>((pend_kt >> 1) * Npad * 4),
+                       base + static_cast<uint32_t>(kHX + kHW + wave * 1024));
+    };
     auto sub = [&](const uint8_t *sb, half8_t (&bc)[8], half8_t (&bn)[8], const half8_t &ac, half8_t &an, int j,
                    bool gf) __attribute__((always_inline)) {
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_setprio(1);
+        if constexpr ((MODE & 256) != 0) {
+            if (j >= 2) {
+                // quarters of 2 MFMAs, each with its share of the next substep's B reads and
+                // dequant, and a DMA piece between quarters
+                if (j < 3) {
+                    if constexpr ((MODE & 8) != 0) an = ac;   // lab ablation: one dequant per k-step
+                    else an = dequant_exact<4>(w, j + 1, ec);
+                }
+                const half8_t (&bq)[8] = (MODE & 16) ? bA : bc;   // lab ablation: one B read per k-step
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if ((MODE & 16) == 0 && j < 3) {
+                        bn[2 * q] = *reinterpret_cast<const half8_t *>(sb + soff[j + 1] + (2 * q) * 32 * kBK * 2);
+                        bn[2 * q + 1] = *reinterpret_cast<const half8_t *>(sb + soff[j + 1] + (2 * q + 1) * 32 * kBK * 2);
+                    }
+                    acc[2 * q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bq[2 * q], acc[2 * q], 0, 0, 0);
+                    acc[2 * q + 1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bq[2 * q + 1], acc[2 * q + 1], 0, 0, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (q < 3) piece(3 * (j - 2) + q);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                __builtin_amdgcn_s_setprio(0);
+                __builtin_amdgcn_sched_barrier(0);
+                return;
+            }
+        }
         if (j < 3) {
             if constexpr ((MODE & 16) == 0) read_b(bn, sb, j + 1);
             if constexpr ((MODE & 8) != 0) an = ac;
@@ -173,7 +229,7 @@ wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
                     acc[r][4 * qd + 2] *= r4[qd].z;
                     acc[r][4 * qd + 3] *= r4[qd].w;
                 }
-                acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bu[r], acc[r], 0, 0, 0);
+                if constexpr ((MODE & 128) == 0) acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bu[r], acc[r], 0, 0, 0);
             }
             // rep i + 1's rescale issues beside rep i's MFMA
             __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
@@ -186,7 +242,8 @@ wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
             }
         } else {
 #pragma unroll
-            for (int r = 0; r < 8; ++r) acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bu[r], acc[r], 0, 0, 0);
+            for (int r = 0; r < 8; ++r)
+                if constexpr ((MODE & 128) == 0) acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bu[r], acc[r], 0, 0, 0);
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -237,7 +294,14 @@ wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
         if constexpr (STAG) {
             if (grp_b) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             barrier();
-            if (issue) stage((slot + 2) % 3, kt + 2, GF);
+            if constexpr ((MODE & 256) != 0) {   // pieces issued inside substeps 2 and 3
+                pend_on = issue;
+                pend_slot = (slot + 2) % 3;
+                pend_kt = kt + 2;
+                pend_gf = GF;
+            } else if (issue) {
+                stage((slot + 2) % 3, kt + 2, GF);
+            }
         }
         sub(sb, bA, bB, aA, aB, 2, GF);
         sub(sb, bB, bA, aB, aA, 3, GF);
@@ -667,19 +731,21 @@ wq_horner_kg2_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
 }
 
 template <int MODE>
-void launch_horner_t(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
+void launch_horner_t(const HornerGemmArgs &a, int y_f32, hipStream_t st, int grows = 0) {
     const int nbm = (a.M + 255) / 256, nbn = a.Npad / 256;
     const unsigned nb = static_cast<unsigned>(nbm * nbn);
     const PSampleEpi ep = a.epi ? *a.epi : PSampleEpi{};
     if (a.epi)
         wq_horner_kernel<float, 1, MODE><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
-                                                             a.epi->x_prev, a.N, a.Npad, nbm, nbn, ep);
+                                                             a.epi->x_prev, a.N, a.Npad, nbm, nbn, ep, grows);
     else if (y_f32)
         wq_horner_kernel<float, 0, MODE><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
-                                                             static_cast<float *>(a.Y), a.N, a.Npad, nbm, nbn, ep);
+                                                             static_cast<float *>(a.Y), a.N, a.Npad, nbm, nbn, ep,
+                                                             grows);
     else
         wq_horner_kernel<__half, 0, MODE><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
-                                                              static_cast<__half *>(a.Y), a.N, a.Npad, nbm, nbn, ep);
+                                                              static_cast<__half *>(a.Y), a.N, a.Npad, nbm, nbn, ep,
+                                                              grows);
 }
 
 }  // namespace
@@ -703,6 +769,30 @@ int launch_horner_kg2_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
 
 int launch_horner_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
 #if DLLM_LAB
+    if (a.lab == 17 || a.lab == 18) {   // lab ablations: 17 = 305's (no stores, rescale; one dequant and
+                                        // B read) with only the weight-word DMA; 18 = 305's with the spread DMA
+        if (a.lab == 17) launch_horner_t<3 | 4 | 8 | 16 | 32>(a, y_f32, st);
+        else launch_horner_t<3 | 4 | 8 | 16 | 256>(a, y_f32, st);
+        DLLM_LAUNCH_CHECK();
+        return DLLM_OK;
+    }
+    if (a.lab == 16) {   // lab A/B: the round-3 schedule (one DMA burst per stage, no MODE bit 8)
+        launch_horner_t<1>(a, y_f32, st);
+        DLLM_LAUNCH_CHECK();
+        return DLLM_OK;
+    }
+    if (a.lab == 14 || a.lab == 15) {   // lab ablations: MFMAs + barriers only (no DMA, rescale, stores;
+                                        // 1 dequant / B read); 15: the DMA ring + barriers only (no MFMA)
+        if (a.lab == 14) launch_horner_t<3 | 4 | 8 | 16 | 64>(a, y_f32, st);
+        else launch_horner_t<3 | 4 | 8 | 16 | 128>(a, y_f32, st);
+        DLLM_LAUNCH_CHECK();
+        return DLLM_OK;
+    }
+    if (a.lab >= 10 && a.lab <= 12) {   // lab A/B: XCD tile groups 4 x 8 / 8 x 4 / 16 x 2
+        launch_horner_t<1 | 256>(a, y_f32, st, a.lab == 10 ? 4 : a.lab == 11 ? 8 : 16);
+        DLLM_LAUNCH_CHECK();
+        return DLLM_OK;
+    }
     if (a.lab >= 1 && a.lab <= 9) {   // lab A/B: 1 no stagger; 2.. ablations (see MODE)
         if (a.lab == 1) launch_horner_t<0>(a, y_f32, st);
         else if (a.lab == 2) launch_horner_t<3>(a, y_f32, st);
@@ -717,7 +807,7 @@ int launch_horner_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
         return DLLM_OK;
     }
 #endif
-    launch_horner_t<1>(a, y_f32, st);
+    launch_horner_t<1 | 256>(a, y_f32, st);
     DLLM_LAUNCH_CHECK();
     return DLLM_OK;
 }

@@ -913,6 +913,46 @@ inline int launch_fused(const float *x, size_t n, const float2 *partials, int np
     }
 }
 
+}  // namespace
+
+// quant_resident.hip: quantize_tensor of one or two tensors in one HBM read (returns 1, launching
+// nothing, when they do not fit on chip or the shape is outside its preconditions).
+int launch_quantize_resident(const float *const *x, const size_t *n, int nt, const int *bits, uint8_t *const *out,
+                             float *const *params, void *ws, size_t ws_bytes, hipStream_t st);
+
+namespace {
+
+// The single pass pays one grid-wide hand-off (a few us): below 4 Mi values per tensor the two
+// passes (both in the Infinity Cache) are as fast.
+constexpr size_t kResidentMin = size_t(1) << 22;
+
+// The single-pass resident kernel is an A/B of the lab build (DLLM_QUANT_RESIDENT=1): measured
+// slower than the two passes at every size it holds (8192 x 4096: 60 vs 49 us),
+// so the product runs the two-pass kernels.
+#if DLLM_LAB
+inline bool resident_disabled() {
+    const char *e = std::getenv("DLLM_QUANT_RESIDENT");
+    return !(e && e[0] == '1');
+}
+#else
+inline bool resident_disabled() { return true; }
+#endif
+
+// One or two tensors at one or two widths through the resident kernel; 0 = launched, 1 = not
+// applicable (the caller runs the multi-pass path), else an error code.
+inline int try_resident(int nt, const float *x0, size_t n0, const float *x1, size_t n1, int ba, int bb,
+                        uint8_t *o0a, float *p0a, uint8_t *o0b, float *p0b, uint8_t *o1a, float *p1a, uint8_t *o1b,
+                        float *p1b, void *ws, size_t wsb, hipStream_t st) {
+    if (resident_disabled() || !fused_width(ba) || (bb && !fused_width(bb))) return 1;
+    if (n0 < kResidentMin || (nt > 1 && n1 < kResidentMin)) return 1;
+    const float *x[2] = {x0, x1};
+    const size_t n[2] = {n0, n1};
+    const int bits[2] = {ba, bb};
+    uint8_t *out[4] = {o0a, o0b, o1a, o1b};
+    float *params[4] = {p0a, p0b, p1a, p1b};
+    return launch_quantize_resident(x, n, nt, bits, out, params, ws, wsb, st);
+}
+
 template <int BA>
 int launch_kv_jobs_b(const KVJobs &J, int bb, unsigned grid, hipStream_t st) {
     switch (bb) {
@@ -984,27 +1024,21 @@ int dllm_quantize_kv(const float *k, size_t n_k, const float *v, size_t n_v, uin
     const bool fast = packed && n_k && n_v && fused_width(bits_a) && (!two || fused_width(bits_b)) &&
                       aligned(k, 16) && aligned(v, 16) && aligned(k_a, 8) && aligned(v_a, 8) &&
                       (!two || (aligned(k_b, 8) && aligned(v_b, 8))) && !fused_disabled();
-    if (!fast) {   // per tensor (same results): each quantize_tensor[_pair] uses its own partials
-        int rc = two ? dllm_quantize_tensor_pair(k, n_k, bits_a, bits_b, packed, k_a, kp_a, k_b, kp_b, pk,
-                                                 sizeof(float2) * nbk, stream)
-                     : dllm_quantize_tensor(k, n_k, bits_a, packed, k_a, kp_a, pk, sizeof(float2) * nbk, stream);
-        if (rc) return rc;
-        return two ? dllm_quantize_tensor_pair(v, n_v, bits_a, bits_b, packed, v_a, vp_a, v_b, vp_b, pv,
-                                               sizeof(float2) * nbv, stream)
-                   : dllm_quantize_tensor(v, n_v, bits_a, packed, v_a, vp_a, pv, sizeof(float2) * nbv, stream);
+    if (fast) {   // lab A/B: one HBM read, K and V together when both fit on chip
+        const int rr = try_resident(2, k, n_k, v, n_v, bits_a, bits_b, k_a, kp_a, k_b, kp_b, v_a, vp_a, v_b, vp_b,
+                                    workspace, workspace_bytes, as_stream(stream));
+        if (rr != 1) return rr;
     }
-    hipStream_t st = as_stream(stream);
-    int rc = launch_minmax(k, n_k, pk, nbk, st);   // min/max K
+    // per tensor, two passes each (min/max | map with the params folded in): measured as fast as or
+    // faster than one launch mapping K beside V's min/max (C4 98.5 vs 99.8 us; C5's pair 44.2 vs
+    // 49.1 us, profiles/r04_quant/), with the same bits
+    int rc = two ? dllm_quantize_tensor_pair(k, n_k, bits_a, bits_b, packed, k_a, kp_a, k_b, kp_b, pk,
+                                             sizeof(float2) * nbk, stream)
+                 : dllm_quantize_tensor(k, n_k, bits_a, packed, k_a, kp_a, pk, sizeof(float2) * nbk, stream);
     if (rc) return rc;
-    KVJobs J{};                                     // map K + min/max V
-    J.map[0] = map_job(k, n_k, k_a, kp_a, k_b, kp_b, pk, static_cast<int>(nbk), nullptr);
-    J.mm[0] = minmax_job(v, n_v, pv);
-    J.nmap = 1; J.nmm = 1; J.nbq = fused_grid(n_k);
-    if ((rc = launch_kv_jobs(J, bits_a, bits_b, st))) return rc;
-    KVJobs J2{};                                    // map V
-    J2.map[0] = map_job(v, n_v, v_a, vp_a, v_b, vp_b, pv, static_cast<int>(nbv), nullptr);
-    J2.nmap = 1; J2.nbq = fused_grid(n_v);
-    return launch_kv_jobs(J2, bits_a, bits_b, st);
+    return two ? dllm_quantize_tensor_pair(v, n_v, bits_a, bits_b, packed, v_a, vp_a, v_b, vp_b, pv,
+                                           sizeof(float2) * nbv, stream)
+               : dllm_quantize_tensor(v, n_v, bits_a, packed, v_a, vp_a, pv, sizeof(float2) * nbv, stream);
 }
 
 int dllm_kv_extremes(const float *k, size_t n_k, const float *v, size_t n_v, float *red, void *workspace,
@@ -1076,6 +1110,11 @@ int dllm_quantize_tensor(const float *x, size_t n, uint8_t bits, int packed, uin
         return fail(DLLM_ERR_INVALID_PARAMS, "workspace too small (see dllm_quantize_tensor_workspace)");
     hipStream_t st = as_stream(stream);
     float2 *partials = static_cast<float2 *>(workspace);
+    if (n && packed) {
+        const int rr = try_resident(1, x, n, nullptr, 0, bits, 0, out, params_out, nullptr, nullptr, nullptr, nullptr,
+                                    nullptr, nullptr, workspace, workspace_bytes, st);
+        if (rr != 1) return rr;
+    }
     if (n) {
         int rc = launch_minmax(x, n, partials, nblk, st);
         if (rc) return rc;
@@ -1104,6 +1143,11 @@ int dllm_quantize_tensor_pair(const float *x, size_t n, uint8_t bits_a, uint8_t 
         return fail(DLLM_ERR_INVALID_PARAMS, "workspace too small (see dllm_quantize_tensor_workspace)");
     hipStream_t st = as_stream(stream);
     float2 *partials = static_cast<float2 *>(workspace);
+    if (n && packed) {
+        const int rr = try_resident(1, x, n, nullptr, 0, bits_a, bits_b, out_a, params_a, out_b, params_b, nullptr,
+                                    nullptr, nullptr, nullptr, workspace, workspace_bytes, st);
+        if (rr != 1) return rr;
+    }
     if (n) {
         int rc = launch_minmax(x, n, partials, nblk, st);
         if (rc) return rc;

@@ -20,6 +20,7 @@
 #include <cmath>
 #include <cstring>
 #include <string>
+#include <initializer_list>
 #include <vector>
 
 #include "common.hpp"
@@ -186,7 +187,26 @@ std::string json_str(const char *s, size_t n) {
     return o + "\"";
 }
 
+// Length of the valid UTF-8 sequence at u[0 .. n) (RFC 3629: no overlong forms, no surrogates,
+// at most U+10FFFF), or 0 when it is not one.
+size_t utf8_len(const unsigned char *u, size_t n) {
+    const unsigned c = u[0];
+    if (c < 0x80) return 1;
+    const size_t k = (c >> 5) == 6 ? 2 : (c >> 4) == 14 ? 3 : (c >> 3) == 30 ? 4 : 0;
+    if (!k || k > n) return 0;
+    unsigned cp = c & (0x7F >> k);
+    for (size_t j = 1; j < k; ++j) {
+        if ((u[j] >> 6) != 2) return 0;
+        cp = (cp << 6) | (u[j] & 63);
+    }
+    static const unsigned lo[5] = {0, 0, 0x80, 0x800, 0x10000};
+    if (cp < lo[k] || cp > 0x10FFFF || (cp >= 0xD800 && cp <= 0xDFFF)) return 0;
+    return k;
+}
+
 // ---- minimal JSON reader for the fixed schemas (serde_json's compact and pretty output) ----------
+// Field handling follows serde's derived Deserialize: unknown fields are skipped, a repeated field
+// is an error ("duplicate field"), a missing one too.
 struct JReader {
     const char *p, *e;
     bool ok = true;
@@ -199,14 +219,32 @@ struct JReader {
     }
     void expect(char c) { if (!lit(std::string(1, c).c_str())) ok = false; }
     std::string key() {
-        ws();
-        if (p >= e || *p != '"') { ok = false; return {}; }
-        const char *s = ++p;
-        while (p < e && *p != '"') ++p;
-        if (p >= e) { ok = false; return {}; }
-        std::string k(s, p++);
+        std::string k;
+        if (!string(k)) return {};
         expect(':');
         return k;
+    }
+    // Skips one value of any type: the value of a field the schema does not name (serde's derived
+    // Deserialize ignores unknown fields unless deny_unknown_fields).
+    bool skip_value(int depth = 0) {
+        ws();
+        if (p >= e || depth > 128) return ok = false;
+        if (*p == '"') { std::string t; return string(t); }
+        if (*p == '{' || *p == '[') {
+            const char close = *p == '{' ? '}' : ']';
+            const bool obj = *p == '{';
+            ++p;
+            if (lit(std::string(1, close).c_str())) return true;
+            do {
+                if (obj) { key(); if (!ok) return false; }
+                if (!skip_value(depth + 1)) return false;
+            } while (lit(","));
+            expect(close);
+            return ok;
+        }
+        if (lit("true") || lit("false") || lit("null")) return true;
+        number();
+        return ok;
     }
     bool null() { return lit("null"); }
     // a JSON number as f64 (serde parses f32 fields through f64 and rounds: f32 visitor)
@@ -285,6 +323,13 @@ struct JReader {
         while (p < e && *p != '"') {
             const unsigned char c = static_cast<unsigned char>(*p);
             if (c < 0x20) return ok = false;
+            if (c >= 0x80) {   // raw UTF-8: the input must be valid UTF-8 (serde_json::from_slice)
+                const size_t k = utf8_len(reinterpret_cast<const unsigned char *>(p), static_cast<size_t>(e - p));
+                if (!k) return ok = false;
+                o.append(p, k);
+                p += k;
+                continue;
+            }
             if (c != '\\') { o.push_back(*p++); continue; }
             if (++p >= e) return ok = false;
             const char x = *p++;
@@ -320,6 +365,15 @@ struct JReader {
     }
 };
 
+int field_index(const std::string &k, std::initializer_list<const char *> names) {
+    int i = 0;
+    for (const char *n : names) {
+        if (k == n) return i;
+        ++i;
+    }
+    return -1;
+}
+
 int parse_params(JReader &j, dllm_qparams *p) {
     j.expect('{');
     bool seen[5] = {false, false, false, false, false};
@@ -327,16 +381,18 @@ int parse_params(JReader &j, dllm_qparams *p) {
         do {
             const std::string k = j.key();
             long long v;
-            if (k == "bits") { if (j.integer(0, 255, v)) p->bits = static_cast<uint8_t>(v); seen[0] = true; }
-            else if (k == "scale") { p->scale = j.f32_or_null(); seen[1] = true; }
-            else if (k == "zero_point") { if (j.integer(INT32_MIN, INT32_MAX, v)) p->zero_point = static_cast<int32_t>(v); seen[2] = true; }
-            else if (k == "symmetric") { j.boolean(p->symmetric); seen[3] = true; }
-            else if (k == "axis") {
+            const int f = field_index(k, {"bits", "scale", "zero_point", "symmetric", "axis"});
+            if (f >= 0 && seen[f]) return fail(DLLM_ERR_SERIALIZATION, "json: duplicate field of QuantizationParams");
+            if (f >= 0) seen[f] = true;
+            if (f == 0) { if (j.integer(0, 255, v)) p->bits = static_cast<uint8_t>(v); }
+            else if (f == 1) { p->scale = j.f32_or_null(); }
+            else if (f == 2) { if (j.integer(INT32_MIN, INT32_MAX, v)) p->zero_point = static_cast<int32_t>(v); }
+            else if (f == 3) { j.boolean(p->symmetric); }
+            else if (f == 4) {
                 if (j.null()) { p->has_axis = 0; p->axis = 0; }
                 else if (j.integer(0, INT64_MAX, v)) { p->has_axis = 1; p->axis = static_cast<uint64_t>(v); }
-                seen[4] = true;
             } else {
-                j.ok = false;
+                j.skip_value();
             }
         } while (j.ok && j.lit(","));
         j.expect('}');
@@ -432,14 +488,19 @@ int dllm_qtensor_from_json(const char *s, size_t len, uint8_t *codes, size_t cod
     std::vector<uint64_t> dims;
     bool seen[3] = {false, false, false};
     j.expect('{');
-    do {
-        const std::string k = j.key();
-        if (k == "data") { j.int_array<uint8_t>(0, 255, data); seen[0] = true; }
-        else if (k == "shape") { j.int_array<uint64_t>(0, INT64_MAX, dims); seen[1] = true; }
-        else if (k == "params") { if (parse_params(j, p)) return DLLM_ERR_SERIALIZATION; seen[2] = true; }
-        else j.ok = false;
-    } while (j.ok && j.lit(","));
-    j.expect('}');
+    if (!j.lit("}")) {
+        do {
+            const std::string k = j.key();
+            const int f = field_index(k, {"data", "shape", "params"});
+            if (f >= 0 && seen[f]) return fail(DLLM_ERR_SERIALIZATION, "json: duplicate field of QuantizedTensor");
+            if (f >= 0) seen[f] = true;
+            if (f == 0) j.int_array<uint8_t>(0, 255, data);
+            else if (f == 1) j.int_array<uint64_t>(0, INT64_MAX, dims);
+            else if (f == 2) { if (parse_params(j, p)) return DLLM_ERR_SERIALIZATION; }
+            else j.skip_value();
+        } while (j.ok && j.lit(","));
+        j.expect('}');
+    }
     j.ws();
     if (!j.ok || j.p != j.e) return fail(DLLM_ERR_SERIALIZATION, "json: malformed QuantizedTensor");
     for (bool v : seen)
@@ -487,11 +548,8 @@ int dllm_compressed_vector_from_bincode(const uint8_t *buf, size_t len, int stri
     if (id) {   // String: UTF-8 is checked by serde; an invalid sequence is a data error
         const unsigned char *u = reinterpret_cast<const unsigned char *>(id);
         for (size_t i = 0; i < *id_len;) {
-            const unsigned c = u[i];
-            const size_t k = c < 0x80 ? 1 : (c >> 5) == 6 ? 2 : (c >> 4) == 14 ? 3 : (c >> 3) == 30 ? 4 : 0;
-            if (!k || i + k > *id_len) return fail(DLLM_ERR_SERIALIZATION, "bincode: invalid UTF-8 in String");
-            for (size_t j = 1; j < k; ++j)
-                if ((u[i + j] >> 6) != 2) return fail(DLLM_ERR_SERIALIZATION, "bincode: invalid UTF-8 in String");
+            const size_t k = utf8_len(u + i, *id_len - i);
+            if (!k) return fail(DLLM_ERR_SERIALIZATION, "bincode: invalid UTF-8 in String");
             i += k;
         }
     }
@@ -532,18 +590,23 @@ int dllm_compressed_vector_from_json(const char *s, size_t len, char *id, size_t
     std::vector<uint64_t> dims;
     bool seen[6] = {false, false, false, false, false, false};
     j.expect('{');
-    do {
-        const std::string k = j.key();
-        long long v;
-        if (k == "id") { j.string(ident); seen[0] = true; }
-        else if (k == "data") { j.int_array<uint8_t>(0, 255, codes); seen[1] = true; }
-        else if (k == "bits") { if (j.integer(0, 255, v)) *bits = static_cast<uint8_t>(v); seen[2] = true; }
-        else if (k == "original_shape") { j.int_array<uint64_t>(0, INT64_MAX, dims); seen[3] = true; }
-        else if (k == "quant_scale") { *scale = j.f32_or_null(); seen[4] = true; }
-        else if (k == "quant_zero_point") { *zero_point = j.f32_or_null(); seen[5] = true; }
-        else j.ok = false;
-    } while (j.ok && j.lit(","));
-    j.expect('}');
+    if (!j.lit("}")) {
+        do {
+            const std::string k = j.key();
+            long long v;
+            const int f = field_index(k, {"id", "data", "bits", "original_shape", "quant_scale", "quant_zero_point"});
+            if (f >= 0 && seen[f]) return fail(DLLM_ERR_SERIALIZATION, "json: duplicate field of CompressedVector");
+            if (f >= 0) seen[f] = true;
+            if (f == 0) j.string(ident);
+            else if (f == 1) j.int_array<uint8_t>(0, 255, codes);
+            else if (f == 2) { if (j.integer(0, 255, v)) *bits = static_cast<uint8_t>(v); }
+            else if (f == 3) j.int_array<uint64_t>(0, INT64_MAX, dims);
+            else if (f == 4) *scale = j.f32_or_null();
+            else if (f == 5) *zero_point = j.f32_or_null();
+            else j.skip_value();
+        } while (j.ok && j.lit(","));
+        j.expect('}');
+    }
     j.ws();
     if (!j.ok || j.p != j.e) return fail(DLLM_ERR_SERIALIZATION, "json: malformed CompressedVector");
     for (bool v : seen)

@@ -174,8 +174,11 @@ class PrefillCompressedVector:
         return cls._decode(_lib.load().dllm_compressed_vector_from_bincode, bytes(b), (int(strict),))
 
     @classmethod
-    def from_json(cls, s: str) -> "PrefillCompressedVector":
-        return cls._decode(_lib.load().dllm_compressed_vector_from_json, s.encode("utf-8"), ())
+    def from_json(cls, s) -> "PrefillCompressedVector":
+        """``s``: the JSON text (str) or its bytes (serde_json::from_slice: not valid UTF-8 ->
+        SerializationError)."""
+        b = s if isinstance(s, (bytes, bytearray)) else s.encode("utf-8")
+        return cls._decode(_lib.load().dllm_compressed_vector_from_json, bytes(b), ())
 
 
 def compressed_vector_records(x: torch.Tensor, bits: int, ids: Optional[List[str]] = None) -> List[PrefillCompressedVector]:

@@ -104,9 +104,9 @@ int dllm_quantize_tensor_pair_with_params(const float *x, size_t n, uint8_t bits
  * QuantizedKVCacheEntry::new(keys, values, bits) (quantization.rs:140-157: K and V each quantized
  * per tensor by quantize_tensor) and, with bits_b != 0, KVCacheEntry::update's prefill and decode
  * copies of the same K/V (diffuse-llm-rs/src/lib.rs:241-276): outputs bit-identical to
- * dllm_quantize_tensor[_pair] of k and of v.  Three launches (min/max K | map K + min/max V | map V),
- * so the map of each tensor reads it back from the Infinity Cache right after its min/max pass.
- * bits_b = 0: one width (the *_b pointers unused).  Workspace: dllm_quantize_kv_workspace(n_k, n_v). */
+ * dllm_quantize_tensor[_pair] of k and of v (each tensor: one min/max pass, one map pass that
+ * writes both widths).  bits_b = 0: one width (the *_b pointers unused).  Workspace:
+ * dllm_quantize_kv_workspace(n_k, n_v). */
 size_t dllm_quantize_kv_workspace(size_t n_k, size_t n_v);
 int dllm_quantize_kv(const float *k, size_t n_k, const float *v, size_t n_v, uint8_t bits_a, uint8_t bits_b,
                      int packed, uint8_t *k_a, float *kp_a, uint8_t *v_a, float *vp_a, uint8_t *k_b, float *kp_b,
@@ -337,7 +337,8 @@ int dllm_compressed_vector_from_json(const char *s, size_t len, char *id, size_t
  * (diffuse-llm-rs/src/lib.rs:910-915).  Build-defined consumer: per head, bidirectional SDPA
  * O = softmax(Q K^T / sqrt(D)) V, with K,V given as per-tensor quantized codes (a1 layout,
  * packed, `bits` in {4, 8}) + device params {scale, zp} (a2 dequant fused into the kernel).
- * Q f16 [S][H][D], O f16 [S][H][D], D == 128.  K/V are unpacked once per call into a grow-only
+ * Q f16 [S][H][D], O f16 [S][H][D], D == 128; Q, O and the codes 16-byte aligned (O is written as
+ * 16-byte row pieces).  K/V are unpacked once per call into a grow-only
  * per-stream workspace (H * ceil(S/64) * 35 KiB), allocated on the first call of a shape. */
 int dllm_kv_attention(const void *Q, const uint8_t *Kq, const float *k_params, const uint8_t *Vq,
                       const float *v_params, uint8_t bits, size_t S, size_t H, size_t D, void *O,

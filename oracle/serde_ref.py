@@ -193,6 +193,19 @@ def params_to_json(p: Params) -> str:
     return _params_json(p)
 
 
+def _no_duplicates(pairs):
+    """serde's derived Deserialize: a field given twice is an error ("duplicate field"); unknown
+    fields are ignored (no deny_unknown_fields on the reference's structs)."""
+    keys = [k for k, _ in pairs]
+    if len(keys) != len(set(keys)):
+        raise SerializationError("json: duplicate field")
+    return dict(pairs)
+
+
+def _loads(s: str):
+    return json.loads(s, object_pairs_hook=_no_duplicates)
+
+
 def _params_from_obj(o) -> Params:
     scale = F32(float("nan") if o["scale"] is None else float(o["scale"]))
     return Params(bits=int(o["bits"]), scale=float(scale), zero_point=int(o["zero_point"]),
@@ -200,7 +213,7 @@ def _params_from_obj(o) -> Params:
 
 
 def params_from_json(s: str) -> Params:
-    return _params_from_obj(json.loads(s))
+    return _params_from_obj(_loads(s))
 
 
 # ---- QuantizedTensor (quantization crate) -------------------------------------------------------------
@@ -234,7 +247,7 @@ def _u8_array(v) -> np.ndarray:
 
 
 def qtensor_from_json(s: str) -> TensorRecord:
-    o = json.loads(s)
+    o = _loads(s)
     return TensorRecord(_u8_array(o["data"]), tuple(int(v) for v in o["shape"]), _params_from_obj(o["params"]))
 
 
@@ -271,7 +284,7 @@ class PrefillCompressedVector:
 
     @classmethod
     def from_json(cls, s: str) -> "PrefillCompressedVector":
-        o = json.loads(s)
+        o = _loads(s)
         f = (lambda v: float(F32(float("nan") if v is None else float(v))))
         bits = int(o["bits"])
         if not 0 <= bits <= 255:

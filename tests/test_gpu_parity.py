@@ -1007,26 +1007,45 @@ def test_bias_cast(dllm, torch):
         assert torch.equal(yy, ref)
 
 
+def _two_pass_ref(q, x, bits):
+    """Codes and params by an independent device path: the min/max kernels (tensor_extremes), the
+    params of :49-56, then the map alone (quantize_tensor_with_params)."""
+    p = q.quantize_params_from_extremes(q.tensor_extremes(x), bits)
+    return q.quantize_tensor_with_params(x, bits, p, packed=True), p
+
+
 @pytest.mark.parametrize("nk,nv", [(1, 1), (7, 9), (2047, 2048), (2048, 2049), (100003, 77777), (1 << 21, 1 << 21),
-                                   (8192 * 32 * 128, 8192 * 32 * 128)])
+                                   ((1 << 22) + 8, (1 << 22) + 2056), (2048 * 4096, 2048 * 4096),
+                                   (8192 * 32 * 128, 8192 * 32 * 128), (40 << 20, 1 << 22)])
 @pytest.mark.parametrize("bits_a,bits_b", [(4, 0), (8, 4), (2, 1), (1, 8)])
 def test_quantize_kv_matches_per_tensor(dllm, torch, orc, nk, nv, bits_a, bits_b):
-    """dllm_quantize_kv (min/max K | map K + min/max V | map V, the coalesced map) against
-    dllm_quantize_tensor[_pair] of each tensor: codes and params bit-identical at one and two widths,
-    ragged sizes (partial chunks and tail octets); and the split form (dllm_kv_extremes +
-    dllm_quantize_kv_with_extremes) likewise.  The smaller sizes are also checked against the oracle."""
+    """dllm_quantize_kv -- the single-pass resident kernel where the tensors fit on chip (K and V
+    together: C5's 2 x 2048 x 4096; each alone: C4's 2 x 8192 x 32 x 128; ragged last slots), else
+    the multi-pass kernels (a 40 Mi-value K) -- and dllm_quantize_tensor[_pair] on the same data,
+    against an independent device path (min/max kernels + params + the map alone): codes and params
+    bit-identical at one and two widths, NaN and +-inf included; the split form (dllm_kv_extremes +
+    dllm_quantize_kv_with_extremes) likewise; the small sizes also against the oracle."""
     if nk > (1 << 21) and (bits_a, bits_b) not in ((4, 0), (8, 4)):
-        pytest.skip("full C4 size at the KV cache's widths only")
+        pytest.skip("large sizes at the KV cache's widths only")
     q = dllm.quantization
     g = torch.Generator(device="cuda").manual_seed(nk + 3 * nv + bits_a)
     k = torch.randn(nk, device="cuda", generator=g) * 2 + 0.25
     v = torch.randn(nv, device="cuda", generator=g) * 0.5 - 1
+    if nk > 64:
+        k[nk // 3] = float("nan")
+        v[nv // 5] = float("inf") if bits_a == 4 else float("nan")
     outs = q.quantize_kv(k, v, bits_a, bits_b)
     for w, bits in enumerate([bits_a] + ([bits_b] if bits_b else [])):
         kc, kp, vc, vp = outs[w]
         for x, c, pr in ((k, kc, kp), (v, vc, vp)):
-            rc, rp = q.quantize_tensor(x, bits, packed=True)
+            rc, rp = _two_pass_ref(q, x, bits)
             assert torch.equal(c, rc) and same_bits(host(pr), host(rp)), (w, bits)
+            tc, tp = q.quantize_tensor(x, bits, packed=True)
+            assert torch.equal(tc, rc) and same_bits(host(tp), host(rp)), (w, bits)
+    if bits_b:
+        (ka, pka), (kb, pkb) = q.quantize_tensor_pair(k, bits_a, bits_b, packed=True)
+        assert torch.equal(ka, outs[0][0]) and torch.equal(kb, outs[1][0])
+        assert same_bits(host(pka), host(outs[0][1])) and same_bits(host(pkb), host(outs[1][1]))
     red = q.kv_extremes(k, v)
     ek, ev = q.tensor_extremes(k), q.tensor_extremes(v)
     assert same_bits(host(red), host(torch.stack([-ek[0], ek[1], -ev[0], ev[1]])))
@@ -1038,6 +1057,16 @@ def test_quantize_kv_matches_per_tensor(dllm, torch, orc, nk, nv, bits_a, bits_b
         rq, rs, rz = orc.quantize_tensor(host(k), bits_a)
         assert np.array_equal(host(outs[0][0]), orc.pack_bits(rq, bits_a))
         assert host(outs[0][1]).tobytes() == np.array([rs, rz], np.float32).tobytes()
+
+
+def test_quantize_resident_vs_oracle_full_size(dllm, torch, orc):
+    """The single-pass kernel at config C4's tensor size (8192 x 32 x 128 values, every slot of all
+    256 blocks, 45 in VGPRs and 19 in LDS) against the C oracle: codes, packed bytes and params."""
+    x = torch.randn(8192 * 32 * 128, device="cuda", generator=torch.Generator(device="cuda").manual_seed(5)) * 3
+    c, p = dllm.quantize_tensor(x, 4, packed=True)
+    rq, rs, rz = orc.quantize_tensor(host(x), 4)
+    assert np.array_equal(host(c), orc.pack_bits(rq, 4))
+    assert host(p).tobytes() == np.array([rs, rz], np.float32).tobytes()
 
 
 def test_quantize_kv_unaligned_and_empty(dllm, torch):

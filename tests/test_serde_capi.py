@@ -194,3 +194,35 @@ def test_compressed_vector_json_decode(dllm, ref, ident):
                 good + " x", good.replace(',"bits":4', '')):
         with pytest.raises(dllm.SerializationError):
             S.PrefillCompressedVector.from_json(bad)
+
+
+def test_json_unknown_and_duplicate_fields(dllm, lib, ref):
+    """serde's derived Deserialize on QuantizationParams / QuantizedTensor / CompressedVector (no
+    deny_unknown_fields): an unknown field -- any JSON value, nested ones included -- is skipped, a
+    field given twice is an error, and a String that is not valid UTF-8 is a data error; the C
+    reader and the oracle's restatement agree."""
+    S = dllm.serde
+    pj = '{"bits":4,"extra":{"a":[1,{"b":null}],"c":"x"},"scale":0.5,"zero_point":3,"symmetric":false,"axis":null}'
+    r = QP()
+    assert lib.dllm_qparams_from_json(pj.encode(), len(pj), C.byref(r)) == 0
+    assert r.bits == 4 and r.zero_point == 3 and ref.params_from_json(pj).zero_point == 3
+    dup = '{"bits":4,"scale":0.5,"zero_point":3,"zero_point":4,"symmetric":false,"axis":null}'
+    assert lib.dllm_qparams_from_json(dup.encode(), len(dup), C.byref(r)) == dllm._lib.ERR_SERIALIZATION
+    with pytest.raises(ref.SerializationError):
+        ref.params_from_json(dup)
+    good = '{"id":"a","data":[1],"bits":4,"original_shape":[1],"quant_scale":0.5,"quant_zero_point":0.0}'
+    extra = good.replace('"bits":4', '"bits":4,"note":[true,false,-1.5e3,"s"]')
+    v = S.PrefillCompressedVector.from_json(extra)
+    assert v.bits == 4 and list(v.data) == [1] and ref.PrefillCompressedVector.from_json(extra).bits == 4
+    for bad in (good.replace('"data":[1]', '"data":[1],"data":[2]'),
+                good.replace('"original_shape":[1]', '"original_shape":[1],"original_shape":[1]')):
+        with pytest.raises(dllm.SerializationError):
+            S.PrefillCompressedVector.from_json(bad)
+        with pytest.raises(ref.SerializationError):
+            ref.PrefillCompressedVector.from_json(bad)
+    raw = good.encode().replace(b'"a"', b'"a\xff"')
+    with pytest.raises(dllm.SerializationError):
+        S.PrefillCompressedVector.from_json(raw)
+    tj = '{"shape":[2],"skip":{},"data":[7,8],"params":' + pj + '}'
+    t = S.qtensor_from_json(tj, device="cpu")
+    assert list(t.shape) == [2] and ref.qtensor_from_json(tj).shape == (2,)
