@@ -160,6 +160,24 @@ wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
     uint32_t w[4];
     float4 r4[4];
     half8_t bA[8], bB[8], aA, aB;
+    // MODE bit 9 (lab ablation, results wrong, timing only): each 32x32x16 MFMA replaced by two
+    // 16x16x32 MFMAs on the same operands (equal FLOPs; the MFMA shape's effect on the held clock)
+    constexpr int kMF = (MODE & 512) ? 2 : 1;
+    typedef float fx4 __attribute__((ext_vector_type(4)));
+    typedef float fx8 __attribute__((ext_vector_type(8)));
+    auto mm = [&](const half8_t &a, const half8_t &b, float16_t &c) __attribute__((always_inline)) {
+        if constexpr ((MODE & 512) != 0) {
+            fx4 c0 = __builtin_shufflevector(c, c, 0, 1, 2, 3);
+            fx4 c1 = __builtin_shufflevector(c, c, 4, 5, 6, 7);
+            c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c0, 0, 0, 0);
+            c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c1, 0, 0, 0);
+            const fx8 lo = __builtin_shufflevector(c0, c1, 0, 1, 2, 3, 4, 5, 6, 7);
+            const fx8 hi = __builtin_shufflevector(c, c, 8, 9, 10, 11, 12, 13, 14, 15);
+            c = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+        } else {
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+        }
+    };
     // MODE bit 8: the pending stage's pieces, issued between MFMA pairs of substeps 2 and 3
     int pend_slot = 0, pend_kt = 0;
     bool pend_gf = false, pend_on = false;
@@ -194,12 +212,12 @@ wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
                         bn[2 * q] = *reinterpret_cast<const half8_t *>(sb + soff[j + 1] + (2 * q) * 32 * kBK * 2);
                         bn[2 * q + 1] = *reinterpret_cast<const half8_t *>(sb + soff[j + 1] + (2 * q + 1) * 32 * kBK * 2);
                     }
-                    acc[2 * q] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bq[2 * q], acc[2 * q], 0, 0, 0);
-                    acc[2 * q + 1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bq[2 * q + 1], acc[2 * q + 1], 0, 0, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    mm(ac, bq[2 * q], acc[2 * q]);
+                    mm(ac, bq[2 * q + 1], acc[2 * q + 1]);
+                    __builtin_amdgcn_sched_group_barrier(0x008, kMF, 0);
                     __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                     __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, kMF, 0);
                     __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                     __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
                     __builtin_amdgcn_sched_barrier(0);
@@ -229,24 +247,24 @@ wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
                     acc[r][4 * qd + 2] *= r4[qd].z;
                     acc[r][4 * qd + 3] *= r4[qd].w;
                 }
-                if constexpr ((MODE & 128) == 0) acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bu[r], acc[r], 0, 0, 0);
+                if constexpr ((MODE & 128) == 0) mm(ac, bu[r], acc[r]);
             }
             // rep i + 1's rescale issues beside rep i's MFMA
             __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 if (i + 1 < 8) __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, kMF, 0);
                 __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                 __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
             }
         } else {
 #pragma unroll
             for (int r = 0; r < 8; ++r)
-                if constexpr ((MODE & 128) == 0) acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bu[r], acc[r], 0, 0, 0);
+                if constexpr ((MODE & 128) == 0) mm(ac, bu[r], acc[r]);
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, kMF, 0);
                 __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                 __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
             }
@@ -730,6 +748,403 @@ wq_horner_kg2_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// The same Horner GEMM on 16x16x32 MFMAs (the product kernel since round 4).  Same block tile, ring,
+// stage bursts, stagger, spread DMA pieces and weight layout as wq_horner_kernel; per wave the
+// 32 columns x 256 tokens are 2 column blocks x 16 token blocks of 16 x 16 (acc = 32 x 4 f32, the
+// same 128 registers).  Why: at equal FLOPs and cycles the chip holds a higher clock on the
+// 16x16x32 shape (MI355X_MICROARCH.md, DVFS give-back item 7) -- the shape-only lab ablation of the
+// round-3 schedule ran 121.7 -> 112.7 us at M = K = N = 4096 (profiles/r04_horner/).
+// A operand: the prefill layout gives lane L column L & 31 and k-chunks 2s + (L >> 5) (8 deep) of
+// substep word s; dequant_exact turns words s = 2h, 2h + 1 into two f16 fragments and ONE
+// v_permlane16_swap per VGPR pair regroups them into the 16x16x32 A fragments of half h: column
+// block 0 (columns 0..15: lane rows R0..R3 hold k-chunks 4h + {0, 2, 1, 3}) and column block 1
+// (columns 16..31, the same chunks).  B operand: token 16 tb + (lane & 15), the k-chunk of the
+// lane's row in the same order, one ds_read_b128 from the swizzled X tile.  D: lane holds columns
+// 16 cb + 4 (lane >> 4) + i of token 16 tb + (lane & 15), so the Horner ratios, the last group's
+// scales and the bias are one float4 per column block.
+typedef float fx4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+// The f16 tile (acc * s + b) through the drained ring as 16-B row chunks, 2 passes of 128 tokens.
+__device__ __forceinline__ void store_tile16_f16_lds(uint8_t *img, const fx4_t (&acc)[16][2], const float4 (&bv)[2],
+                                                     __half *Y, int N, int m0, int n0, int wave, int lane) {
+    constexpr int kRowB = 512, kCpr = 32;
+    const int row16 = lane & 15, rq = lane >> 4;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int t = 16 * i + row16;
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb) {
+                const int pc = (4 * wave + 2 * cb + (rq >> 1)) ^ (t & (kCpr - 1));
+                const fx4_t &a = acc[8 * p + i][cb];
+                const float4 &b = bv[cb];
+                union { __half h[4]; uint2 u; } pk;
+                pk.h[0] = __float2half_rn(a[0] + b.x);
+                pk.h[1] = __float2half_rn(a[1] + b.y);
+                pk.h[2] = __float2half_rn(a[2] + b.z);
+                pk.h[3] = __float2half_rn(a[3] + b.w);
+                *reinterpret_cast<uint2 *>(img + t * kRowB + pc * 16 + (rq & 1) * 8) = pk.u;
+            }
+        }
+        __syncthreads();
+        const int c = lane % kCpr;
+#pragma unroll
+        for (int t0 = wave * 2; t0 < 128; t0 += 16) {
+            const int t = t0 + lane / kCpr;
+            const uint4 v = *reinterpret_cast<const uint4 *>(img + t * kRowB + ((c ^ (t & (kCpr - 1))) * 16));
+#if DLLM_NT_STORE
+            typedef unsigned int u4nt __attribute__((ext_vector_type(4)));
+            __builtin_nontemporal_store(u4nt{v.x, v.y, v.z, v.w},
+                                        reinterpret_cast<u4nt *>(Y + static_cast<size_t>(m0 + 128 * p + t) * N + n0 + 8 * c));
+#else
+            *reinterpret_cast<uint4 *>(Y + static_cast<size_t>(m0 + 128 * p + t) * N + n0 + 8 * c) = v;
+#endif
+        }
+        __syncthreads();
+    }
+}
+
+template <typename YT, int EPI, int MODE>
+__global__ void __launch_bounds__(512, 1)
+wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdev,
+                   const uint32_t *__restrict__ sz, const float *__restrict__ hr, const float *__restrict__ sf,
+                   const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad, int nbm, int nbn,
+                   PSampleEpi epi) {
+    constexpr bool STAG = MODE & 1;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[3 * kHStage];
+
+    // XCD-aware bijective remap (as wq_horner_kernel)
+    const int nb = nbm * nbn, orig = blockIdx.x;
+    const int xcd = orig % kXCDs, q8 = nb / kXCDs, r8 = nb % kXCDs;
+    const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / kXCDs;
+    const int bm = tile / nbn, bn = tile % nbn;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int m0 = bm * 256, n0 = bn * 256;
+    const int nk = K / kBK;
+
+    uint32_t xo[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int row = (i * 8 + wave) * 8 + (lane >> 3);
+        const int rrow = (m0 + row < M ? m0 + row : M - 1) - m0;
+        const int c = (lane & 7) ^ ((row >> 1) & 7);
+        xo[i] = static_cast<uint32_t>((rrow * K + c * 8) * 2);
+    }
+    const __amdgpu_buffer_rsrc_t xr = raw_rsrc(X + static_cast<size_t>(m0) * K);
+    const uint32_t nt = static_cast<uint32_t>(n0 + 32 * wave) >> 5;
+    const __amdgpu_buffer_rsrc_t wr = raw_rsrc(wdev + static_cast<size_t>(nt) * nk * 64 * 4);
+    const uint32_t wo = static_cast<uint32_t>(lane * 16);
+    const __amdgpu_buffer_rsrc_t gr =
+        raw_rsrc(wave == 0 ? static_cast<const void *>(sz + n0) : static_cast<const void *>(hr + n0));
+    const bool has_g = wave < 2;
+    const uint32_t sbase = __builtin_amdgcn_readfirstlane(lds_addr(smem));
+
+    auto stage = [&](int slot, int kt, bool gf) __attribute__((always_inline)) {
+        const uint32_t base = sbase + static_cast<uint32_t>(slot * kHStage);
+        horner_burst(xr, xo[0], xo[1], xo[2], xo[3], static_cast<uint32_t>(kt * kBK * 2), wr, wo,
+                     static_cast<uint32_t>(kt * 1024), base + static_cast<uint32_t>(wave * 1024));
+        if (gf && has_g)
+            blds16_asm(gr, wo, static_cast<uint32_t>((kt >> 1) * Npad * 4),
+                       base + static_cast<uint32_t>(kHX + kHW + wave * 1024));
+    };
+
+    fx4_t acc[16][2];
+#pragma unroll
+    for (int t = 0; t < 16; ++t)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) acc[t][cb] = fx4_t{0.f, 0.f, 0.f, 0.f};
+
+    const int row16 = lane & 15, rq = lane >> 4;
+    const int cq = ((rq & 1) << 1) | (rq >> 1);   // k-chunk of lane row rq after the swap: 0, 2, 1, 3
+    int soff[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) soff[h] = row16 * (kBK * 2) + (((4 * h + cq) ^ ((row16 >> 1) & 7)) << 4);
+
+    // B fragments of substep j (half j >> 1, token blocks 8 (j & 1) .. + 7)
+    auto read_b = [&](half8_t (&b)[8], const uint8_t *sb, int j) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            b[i] = *reinterpret_cast<const half8_t *>(sb + soff[j >> 1] + (8 * (j & 1) + i) * 16 * kBK * 2);
+    };
+
+    ExactConsts ec;
+    uint32_t w[4];
+    float4 r4[2];
+    half8_t bA[8], bB[8], a00, a01, a10, a11;
+    // A fragments of half h (words 2h, 2h + 1) for column blocks 0 and 1
+    auto make_a = [&](int h, half8_t &c0, half8_t &c1) __attribute__((always_inline)) {
+        u32x4_t u0 = __builtin_bit_cast(u32x4_t, dequant_exact<4>(w, 2 * h, ec));
+        u32x4_t u1 = __builtin_bit_cast(u32x4_t, dequant_exact<4>(w, 2 * h + 1, ec));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const auto r = __builtin_amdgcn_permlane16_swap(u0[e], u1[e], false, false);
+            u0[e] = r[0];
+            u1[e] = r[1];
+        }
+        c0 = __builtin_bit_cast(half8_t, u0);
+        c1 = __builtin_bit_cast(half8_t, u1);
+    };
+    int pend_slot = 0, pend_kt = 0;
+    bool pend_gf = false, pend_on = false;
+    auto piece = [&](int p) __attribute__((always_inline)) {
+        if (!pend_on) return;
+        const uint32_t base = sbase + static_cast<uint32_t>(pend_slot * kHStage);
+        if (p < 4)
+            blds16_asm(xr, xo[p], static_cast<uint32_t>(pend_kt * kBK * 2),
+                       base + static_cast<uint32_t>(wave * 1024 + p * 0x2000));
+        else if (p == 4)
+            blds16_asm(wr, wo, static_cast<uint32_t>(pend_kt * 1024), base + static_cast<uint32_t>(kHX + wave * 1024));
+        else if (pend_gf && has_g)
+            blds16_asm(gr, wo, static_cast<uint32_t>((pend_kt >> 1) * Npad * 4),
+                       base + static_cast<uint32_t>(kHX + kHW + wave * 1024));
+    };
+    auto mma = [&](int t, int cb, const half8_t &a, const half8_t &b) __attribute__((always_inline)) {
+        acc[t][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, acc[t][cb], 0, 0, 0);
+    };
+    auto rescale = [&](int t) __attribute__((always_inline)) {
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+            acc[t][cb][0] *= r4[cb].x;
+            acc[t][cb][1] *= r4[cb].y;
+            acc[t][cb][2] *= r4[cb].z;
+            acc[t][cb][3] *= r4[cb].w;
+        }
+    };
+    // Substep j: 16 MFMAs (token blocks 8 (j & 1) + i, both column blocks) of half j >> 1; the next
+    // substep's B fragments; substep 2 starts with the A fragments of half 1.
+    auto sub = [&](const uint8_t *sb, half8_t (&bc)[8], half8_t (&bn)[8], int j, bool gf) __attribute__((always_inline)) {
+        const int tb0 = 8 * (j & 1);
+        const half8_t &a0 = j < 2 ? a00 : a10;
+        const half8_t &a1 = j < 2 ? a01 : a11;
+        __builtin_amdgcn_sched_barrier(0);
+        if (j == 2) {   // half 1's A fragments once half 0's are dead (register budget)
+            make_a(1, a10, a11);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        __builtin_amdgcn_s_setprio(1);
+        if ((MODE & 256) != 0 && j >= 2) {
+            // quarters of 4 MFMAs (2 token blocks), each with 2 of the next substep's B reads, and a
+            // DMA piece between quarters
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (j < 3) {
+                    bn[2 * q] = *reinterpret_cast<const half8_t *>(sb + soff[(j + 1) >> 1] + (8 * ((j + 1) & 1) + 2 * q) * 16 * kBK * 2);
+                    bn[2 * q + 1] = *reinterpret_cast<const half8_t *>(sb + soff[(j + 1) >> 1] + (8 * ((j + 1) & 1) + 2 * q + 1) * 16 * kBK * 2);
+                }
+                mma(tb0 + 2 * q, 0, a0, bc[2 * q]);
+                mma(tb0 + 2 * q, 1, a1, bc[2 * q]);
+                mma(tb0 + 2 * q + 1, 0, a0, bc[2 * q + 1]);
+                mma(tb0 + 2 * q + 1, 1, a1, bc[2 * q + 1]);
+                __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                if (q < 3) piece(3 * (j - 2) + q);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_sched_barrier(0);
+            return;
+        }
+        if (j < 3) read_b(bn, sb, j + 1);
+        if (gf && j < 2) {
+            // acc <- acc * r_g right before each token block's first MFMA of the group (block i + 1's
+            // rescale beside block i's MFMAs)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                rescale(tb0 + i);
+                mma(tb0 + i, 0, a0, bc[i]);
+                mma(tb0 + i, 1, a1, bc[i]);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                if (i + 1 < 8) __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                mma(tb0 + i, 0, a0, bc[i]);
+                mma(tb0 + i, 1, a1, bc[i]);
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+            }
+        }
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto barrier = []() __attribute__((always_inline)) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    const bool grp_b = STAG && wave >= 4;
+    auto step = [&](int slot, int kt, auto gf_tag) __attribute__((always_inline)) {
+        constexpr bool GF = decltype(gf_tag)::value;
+        const bool issue = kt + 2 < nk;
+        if (!STAG && issue) stage((slot + 2) % 3, kt + 2, GF);
+        const uint8_t *sb = smem + slot * kHStage;
+        {
+            const uint4 v = *reinterpret_cast<const uint4 *>(sb + kHX + wave * 1024 + lane * 16);
+            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+        }
+        if constexpr (GF) {
+            half2_t nz, sc;
+            split_sz(*reinterpret_cast<const uint32_t *>(sb + kHX + kHW + (wave * 32 + (lane & 31)) * 4), nz, sc);
+            ec = exact_consts(nz);
+            const float *rl = reinterpret_cast<const float *>(sb + kHX + kHW + 1024) + wave * 32 + 4 * rq;
+            r4[0] = *reinterpret_cast<const float4 *>(rl);
+            r4[1] = *reinterpret_cast<const float4 *>(rl + 16);
+        }
+        read_b(bA, sb, 0);
+        make_a(0, a00, a01);
+        sub(sb, bA, bB, 0, GF);
+        sub(sb, bB, bA, 1, GF);
+        if constexpr (STAG) {
+            if (grp_b) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            barrier();
+            if constexpr ((MODE & 256) != 0) {
+                pend_on = issue;
+                pend_slot = (slot + 2) % 3;
+                pend_kt = kt + 2;
+                pend_gf = GF;
+            } else if (issue) {
+                stage((slot + 2) % 3, kt + 2, GF);
+            }
+        }
+        sub(sb, bA, bB, 2, GF);
+        sub(sb, bB, bA, 3, GF);
+        if (!grp_b) {
+            if (issue) {
+                if (GF && has_g) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        }
+        barrier();
+    };
+
+    stage(0, 0, true);
+    stage(1, 1, false);
+    asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (grp_b) barrier();
+    using GFt = std::integral_constant<bool, true>;
+    using GFf = std::integral_constant<bool, false>;
+    for (int kt = 0; kt < nk; kt += 6) {
+        step(0, kt, GFt{});
+        step(1, kt + 1, GFf{});
+        if (kt + 2 < nk) {
+            step(2, kt + 2, GFt{});
+            step(0, kt + 3, GFf{});
+        }
+        if (kt + 4 < nk) {
+            step(1, kt + 4, GFt{});
+            step(2, kt + 5, GFf{});
+        }
+    }
+    if (STAG && !grp_b) barrier();
+
+    // acc = sum_g T_g s_g / s_{G-1}: times the last group's scales, then the bias
+    const int nc0 = n0 + wave * 32 + 4 * rq;   // + 16 cb: the lane's 4 columns of column block cb
+    const float *sl = sf + static_cast<size_t>(nk / 2 - 1) * Npad + nc0;
+    float4 bv[2];
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+        const float4 s = *reinterpret_cast<const float4 *>(sl + 16 * cb);
+        bv[cb] = *reinterpret_cast<const float4 *>(bias + nc0 + 16 * cb);
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            acc[t][cb][0] *= s.x;
+            acc[t][cb][1] *= s.y;
+            acc[t][cb][2] *= s.z;
+            acc[t][cb][3] *= s.w;
+        }
+    }
+    if constexpr ((MODE & 2) != 0) {   // lab ablation: keep the results live, store nothing
+#pragma unroll
+        for (int t = 0; t < 16; ++t)
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb) asm volatile("" ::"v"(acc[t][cb]));
+        return;
+    }
+    if constexpr (EPI == 1) {
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const int m = m0 + 16 * t + row16;
+            if (m >= M) continue;
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb) {
+                if (nc0 + 16 * cb >= N) continue;
+                psample4(epi, m, nc0 + 16 * cb, N, acc[t][cb][0] + bv[cb].x, acc[t][cb][1] + bv[cb].y,
+                         acc[t][cb][2] + bv[cb].z, acc[t][cb][3] + bv[cb].w);
+            }
+        }
+        return;
+    }
+    const bool full = (m0 + 256 <= M) && (n0 + 256 <= N) && (N % 4) == 0;
+    if constexpr (std::is_same<YT, __half>::value) {
+        if (full && (N % 8) == 0) {   // coalesced 16-B row stores through the drained ring
+            store_tile16_f16_lds(smem, acc, bv, Y, N, m0, n0, wave, lane);
+            return;
+        }
+    }
+    if (full) {
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            YT *yrow = Y + static_cast<size_t>(m0 + 16 * t + row16) * N + nc0;
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb)
+                store4<YT>(yrow + 16 * cb, acc[t][cb][0] + bv[cb].x, acc[t][cb][1] + bv[cb].y,
+                           acc[t][cb][2] + bv[cb].z, acc[t][cb][3] + bv[cb].w);
+        }
+    } else {
+        const bool vec_ok = (N % 4) == 0;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const int m = m0 + 16 * t + row16;
+            if (m >= M) continue;
+            YT *yrow = Y + static_cast<size_t>(m) * N;
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb)
+                store_out4<YT>(yrow, bias, nc0 + 16 * cb, N, vec_ok, acc[t][cb][0], acc[t][cb][1], acc[t][cb][2],
+                               acc[t][cb][3]);
+        }
+    }
+}
+
+template <int MODE>
+void launch_horner16_t(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
+    const int nbm = (a.M + 255) / 256, nbn = a.Npad / 256;
+    const unsigned nb = static_cast<unsigned>(nbm * nbn);
+    const PSampleEpi ep = a.epi ? *a.epi : PSampleEpi{};
+    if (a.epi)
+        wq_horner16_kernel<float, 1, MODE><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
+                                                               a.epi->x_prev, a.N, a.Npad, nbm, nbn, ep);
+    else if (y_f32)
+        wq_horner16_kernel<float, 0, MODE><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
+                                                               static_cast<float *>(a.Y), a.N, a.Npad, nbm, nbn, ep);
+    else
+        wq_horner16_kernel<__half, 0, MODE><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
+                                                                static_cast<__half *>(a.Y), a.N, a.Npad, nbm, nbn, ep);
+}
+
 template <int MODE>
 void launch_horner_t(const HornerGemmArgs &a, int y_f32, hipStream_t st, int grows = 0) {
     const int nbm = (a.M + 255) / 256, nbn = a.Npad / 256;
@@ -769,6 +1184,17 @@ int launch_horner_kg2_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
 
 int launch_horner_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
 #if DLLM_LAB
+    if (a.lab == 21) {   // lab A/B: the round-3 MFMA shape (32x32x16) with the product schedule
+        launch_horner_t<1 | 256>(a, y_f32, st);
+        DLLM_LAUNCH_CHECK();
+        return DLLM_OK;
+    }
+    if (a.lab == 19 || a.lab == 20) {   // lab ablations: the MFMA shape (MODE bit 9) in the product
+        // schedule (19) and in the MFMAs-only skeleton of 14 (20)
+        if (a.lab == 19) launch_horner_t<1 | 256 | 512>(a, y_f32, st);
+        else launch_horner_t<3 | 4 | 8 | 16 | 64 | 512>(a, y_f32, st);
+        return DLLM_OK;
+    }
     if (a.lab == 17 || a.lab == 18) {   // lab ablations: 17 = 305's (no stores, rescale; one dequant and
                                         // B read) with only the weight-word DMA; 18 = 305's with the spread DMA
         if (a.lab == 17) launch_horner_t<3 | 4 | 8 | 16 | 32>(a, y_f32, st);
@@ -807,7 +1233,7 @@ int launch_horner_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
         return DLLM_OK;
     }
 #endif
-    launch_horner_t<1 | 256>(a, y_f32, st);
+    launch_horner16_t<1 | 256>(a, y_f32, st);
     DLLM_LAUNCH_CHECK();
     return DLLM_OK;
 }

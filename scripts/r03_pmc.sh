@@ -1,12 +1,12 @@
 #!/bin/bash
-# PMC passes on the bench GEMM (M = K = N = 4096, the default kernel: wq_horner_kernel): the SQ
+# PMC passes on the bench GEMM (M = K = N = 4096, the default kernel: wq_horner16_kernel): the SQ
 # wait/issue breakdown, instruction mix, clock, and HBM traffic (FETCH_SIZE doubled per the gfx950
 # calibration + WRITE_SIZE), each counter set in its own rocprofv3 run.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT="$PWD/gpurun_out/pmc"; mkdir -p "$OUT"
-KRE=${KREGEX:-wq_horner_kernel}
+KRE=${KREGEX:-wq_horner16_kernel}
 i=0
 for C in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \
          "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS" \
@@ -17,4 +17,4 @@ for C in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_I
   rc=$?; echo "pass $i rc=$rc"
   [ $rc -eq 0 ] || exit $rc
 done
-python3 scripts/pmc_to_json.py "$OUT" "$OUT/pmc_gemm.json" wq_horner_kernel 4096 4096 4096 4 128 "${GEMM_REV:-r03-horner-nt}"
+python3 scripts/pmc_to_json.py "$OUT" "$OUT/pmc_gemm.json" "$KRE" 4096 4096 4096 4 128 "${GEMM_REV:-r04-horner16}"

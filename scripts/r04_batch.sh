@@ -29,7 +29,21 @@ for s in ${STEPS:-tests chain quant horner shard}; do
             for v in -1 310 311 312; do
               step pmc_fetch_$v 90 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex wq_horner -d $O/pmc_fetch_$v -o pmc --output-format csv -- python scripts/horner_ab.py $v
             done;;
+    clock) for v in ${CLOCKV:--1 314 315 305 317}; do
+             step clk_$v 90 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES --kernel-include-regex wq_horner -d $O/clk_$v -o pmc --output-format csv -- python scripts/horner_ab.py $v
+           done;;
+    clkshard) i=0
+           for C in "GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVES SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA" "FETCH_SIZE" "SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"; do
+             i=$((i+1))
+             LIBS=diffusion-llm-rs_amd/lib/libdllm_hip.so ROUNDS=1 SHAPES=${CSHAPES:-4096:1024,4096:512,4096:4096} step clkshard_$i 120 rocprofv3 --pmc $C --kernel-include-regex "wq_gemm_exact|wq_horner" -d $O/clkshard_$i -o pmc --output-format csv -- python scripts/gemm_ab.py
+           done;;
+    shape) step shape 200 python scripts/horner_ab.py -1 319 314 320;;
+    h16) step h16 200 python scripts/horner_ab.py -1 321 -1 321;;
+    blas) step blas 120 python scripts/blas_shapes.py
+          LIBS=diffusion-llm-rs_amd/lib/libdllm_hip.so ROUNDS=2 step shard_ab 200 python scripts/gemm_ab.py;;
     tp) DLLM_BENCH_BACKEND=gloo step tp_trace 400 rocprofv3 --kernel-trace -d $O/tp -o kt --output-format csv -- python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --tp-steps 4 --no-cpu;;
+    tpstep) DLLM_BENCH_BACKEND=gloo step tp_step 300 rocprofv3 --kernel-trace -d $O/tpstep -o kt --output-format csv -- python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29535 scripts/tp_step_trace.py
+            for f in $(ls $O/tpstep/*kernel_trace.csv 2>/dev/null); do python scripts/tp_step_trace.py --analyze $f > $O/tp_step_kernels.json; done;;
     pmcm) for m in 64 256; do
             k=$([ $m -le 64 ] && echo wq_decode || echo wq_gemm_exact)
             i=0
