@@ -320,6 +320,9 @@ struct HornerGemmArgs {
     int lab = 0;   // lab build only: 1 = the unstaggered schedule (A/B); 2 / 3 = staggered / not, no stores
 };
 int launch_horner_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st);
+// The same kernel on 128- or 64-token x 256-column tiles (rows = 128 / 64: grids where larger tiles
+// leave CUs idle).
+int launch_horner_rows_gemm(const HornerGemmArgs &a, int rows, int y_f32, hipStream_t st);
 // The same Horner form on 256 x 128 tiles with two k-groups per tile (linear_horner.hip): needs
 // K % 256 == 0 and Npad % 128 == 0.
 int launch_horner_kg2_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st);

@@ -766,20 +766,22 @@ wq_horner_kg2_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
 typedef float fx4_t __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
-// The f16 tile (acc * s + b) through the drained ring as 16-B row chunks, 2 passes of 128 tokens.
-__device__ __forceinline__ void store_tile16_f16_lds(uint8_t *img, const fx4_t (&acc)[16][2], const float4 (&bv)[2],
+// The f16 tile (acc * s + b) through the drained ring as 16-B row chunks, passes of 128 tokens.
+template <int TB>
+__device__ __forceinline__ void store_tile16_f16_lds(uint8_t *img, const fx4_t (&acc)[TB][2], const float4 (&bv)[2],
                                                      __half *Y, int N, int m0, int n0, int wave, int lane) {
     constexpr int kRowB = 512, kCpr = 32;
     const int row16 = lane & 15, rq = lane >> 4;
+    constexpr int kTPP = TB < 8 ? TB : 8;   // token blocks per pass (128 rows at most)
 #pragma unroll
-    for (int p = 0; p < 2; ++p) {
+    for (int p = 0; p < TB / kTPP; ++p) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < kTPP; ++i) {
             const int t = 16 * i + row16;
 #pragma unroll
             for (int cb = 0; cb < 2; ++cb) {
                 const int pc = (4 * wave + 2 * cb + (rq >> 1)) ^ (t & (kCpr - 1));
-                const fx4_t &a = acc[8 * p + i][cb];
+                const fx4_t &a = acc[kTPP * p + i][cb];
                 const float4 &b = bv[cb];
                 union { __half h[4]; uint2 u; } pk;
                 pk.h[0] = __float2half_rn(a[0] + b.x);
@@ -792,29 +794,49 @@ __device__ __forceinline__ void store_tile16_f16_lds(uint8_t *img, const fx4_t (
         __syncthreads();
         const int c = lane % kCpr;
 #pragma unroll
-        for (int t0 = wave * 2; t0 < 128; t0 += 16) {
+        for (int t0 = wave * 2; t0 < 16 * kTPP; t0 += 16) {
             const int t = t0 + lane / kCpr;
             const uint4 v = *reinterpret_cast<const uint4 *>(img + t * kRowB + ((c ^ (t & (kCpr - 1))) * 16));
 #if DLLM_NT_STORE
             typedef unsigned int u4nt __attribute__((ext_vector_type(4)));
             __builtin_nontemporal_store(u4nt{v.x, v.y, v.z, v.w},
-                                        reinterpret_cast<u4nt *>(Y + static_cast<size_t>(m0 + 128 * p + t) * N + n0 + 8 * c));
+                                        reinterpret_cast<u4nt *>(Y + static_cast<size_t>(m0 + 16 * kTPP * p + t) * N + n0 + 8 * c));
 #else
-            *reinterpret_cast<uint4 *>(Y + static_cast<size_t>(m0 + 128 * p + t) * N + n0 + 8 * c) = v;
+            *reinterpret_cast<uint4 *>(Y + static_cast<size_t>(m0 + 16 * kTPP * p + t) * N + n0 + 8 * c) = v;
 #endif
         }
         __syncthreads();
     }
 }
 
-template <typename YT, int EPI, int MODE>
+// TB = 16: 256-token tiles (the M = 4096 grid), a stage = one 64-deep k-step.  TB = 8: 128-token
+// tiles (grids where 256 x 256 tiles leave CUs idle and 128 x 256 fill them: M = 2048 at N = 4096,
+// the 2-GPU column shard at M = 4096), a stage = one 128-deep group (two k-steps: X 2 x 16 KiB,
+// weight words 2 x 8 KiB) so that a stage carries the same 64 MFMAs per wave as at TB = 16 and the
+// 3-stage ring hides the same DMA latency.  Either way a stage is 4 substeps of 16 MFMAs:
+// TB = 16: substep j = (half j >> 1, token blocks 8 (j & 1) ..); TB = 8: (k-step j >> 1, half j & 1).
+template <int TB>
+struct H16 {
+    static_assert(TB == 16 || TB == 8, "256- or 128-token tiles");
+    static constexpr int kKPS = 16 / TB;                  // 64-deep k-steps per stage
+    static constexpr int kXB = 32 * 1024;                  // X bytes per stage (kKPS sub-tiles of 16 TB rows x 64)
+    static constexpr int kXSub = kXB / kKPS;               // one k-step's X sub-tile
+    static constexpr int kWB = kKPS * kHW;                 // weight words per stage
+    static constexpr int kStage = kXB + kWB + kHG;         // 43008 / 51200 B
+    static constexpr int kNX = TB / 4;                     // X pieces per wave per k-step sub-tile
+    static constexpr int kPieces = kKPS * (kNX + 1) + 1;   // DMA pieces per stage (X, W, group data)
+};
+
+template <typename YT, int EPI, int MODE, int TB = 16>
 __global__ void __launch_bounds__(512, 1)
 wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdev,
                    const uint32_t *__restrict__ sz, const float *__restrict__ hr, const float *__restrict__ sf,
                    const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad, int nbm, int nbn,
                    PSampleEpi epi) {
     constexpr bool STAG = MODE & 1;
-    __shared__ __attribute__((aligned(16))) uint8_t smem[3 * kHStage];
+    using L = H16<TB>;
+    constexpr int kStage = L::kStage, kXB = L::kXB, kKPS = L::kKPS;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[3 * kStage];
 
     // XCD-aware bijective remap (as wq_horner_kernel)
     const int nb = nbm * nbn, orig = blockIdx.x;
@@ -823,12 +845,13 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
     const int bm = tile / nbn, bn = tile % nbn;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int m0 = bm * 256, n0 = bn * 256;
-    const int nk = K / kBK;
+    const int m0 = bm * 16 * TB, n0 = bn * 256;
+    const int nk = K / kBK;              // 64-deep k-steps
+    const int ns = nk / kKPS;            // stages
 
-    uint32_t xo[4];
+    uint32_t xo[L::kNX];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < L::kNX; ++i) {
         const int row = (i * 8 + wave) * 8 + (lane >> 3);
         const int rrow = (m0 + row < M ? m0 + row : M - 1) - m0;
         const int c = (lane & 7) ^ ((row >> 1) & 7);
@@ -843,18 +866,38 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
     const bool has_g = wave < 2;
     const uint32_t sbase = __builtin_amdgcn_readfirstlane(lds_addr(smem));
 
-    auto stage = [&](int slot, int kt, bool gf) __attribute__((always_inline)) {
-        const uint32_t base = sbase + static_cast<uint32_t>(slot * kHStage);
-        horner_burst(xr, xo[0], xo[1], xo[2], xo[3], static_cast<uint32_t>(kt * kBK * 2), wr, wo,
-                     static_cast<uint32_t>(kt * 1024), base + static_cast<uint32_t>(wave * 1024));
-        if (gf && has_g)
-            blds16_asm(gr, wo, static_cast<uint32_t>((kt >> 1) * Npad * 4),
-                       base + static_cast<uint32_t>(kHX + kHW + wave * 1024));
+    // DMA piece p of stage st into ring slot `slot`: X pieces (sub-tile p / kNX, piece p % kNX), then
+    // the weight words of each k-step, then (group-first stages, waves 0 and 1) the group data.
+    auto piece = [&](int p, int slot, int st, bool gf) __attribute__((always_inline)) {
+        const uint32_t base = sbase + static_cast<uint32_t>(slot * kStage);
+        constexpr int nxp = kKPS * L::kNX;
+        if (p < nxp) {
+            const int kk = p / L::kNX, i = p % L::kNX;
+            blds16_asm(xr, xo[i], static_cast<uint32_t>((st * kKPS + kk) * kBK * 2),
+                       base + static_cast<uint32_t>(kk * L::kXSub + wave * 1024 + i * 0x2000));
+        } else if (p < nxp + kKPS) {
+            const int kk = p - nxp;
+            blds16_asm(wr, wo, static_cast<uint32_t>((st * kKPS + kk) * 1024),
+                       base + static_cast<uint32_t>(kXB + kk * kHW + wave * 1024));
+        } else if (p == nxp + kKPS && gf && has_g) {
+            blds16_asm(gr, wo, static_cast<uint32_t>(((st * kKPS) >> 1) * Npad * 4),
+                       base + static_cast<uint32_t>(kXB + L::kWB + wave * 1024));
+        }
+    };
+    auto stage = [&](int slot, int st, bool gf) __attribute__((always_inline)) {
+        if constexpr (TB == 16) {
+            horner_burst(xr, xo[0], xo[1], xo[2], xo[3], static_cast<uint32_t>(st * kBK * 2), wr, wo,
+                         static_cast<uint32_t>(st * 1024), sbase + static_cast<uint32_t>(slot * kStage + wave * 1024));
+            piece(L::kPieces - 1, slot, st, gf);
+        } else {
+#pragma unroll
+            for (int p = 0; p < L::kPieces; ++p) piece(p, slot, st, gf);
+        }
     };
 
-    fx4_t acc[16][2];
+    fx4_t acc[TB][2];
 #pragma unroll
-    for (int t = 0; t < 16; ++t)
+    for (int t = 0; t < TB; ++t)
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) acc[t][cb] = fx4_t{0.f, 0.f, 0.f, 0.f};
 
@@ -864,17 +907,26 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
 #pragma unroll
     for (int h = 0; h < 2; ++h) soff[h] = row16 * (kBK * 2) + (((4 * h + cq) ^ ((row16 >> 1) & 7)) << 4);
 
-    // B fragments of substep j (half j >> 1, token blocks 8 (j & 1) .. + 7)
+    // substep j -> (k-step kk of the stage, half h, first token block tb0)
+    auto sj_kk = [](int j) { return TB == 16 ? 0 : (j >> 1); };
+    auto sj_h = [](int j) { return TB == 16 ? (j >> 1) : (j & 1); };
+    auto sj_tb0 = [](int j) { return TB == 16 ? 8 * (j & 1) : 0; };
+    // B fragments of substep j
     auto read_b = [&](half8_t (&b)[8], const uint8_t *sb, int j) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < 8; ++i)
-            b[i] = *reinterpret_cast<const half8_t *>(sb + soff[j >> 1] + (8 * (j & 1) + i) * 16 * kBK * 2);
+            b[i] = *reinterpret_cast<const half8_t *>(sb + sj_kk(j) * L::kXSub + soff[sj_h(j)] +
+                                                      (sj_tb0(j) + i) * 16 * kBK * 2);
     };
 
     ExactConsts ec;
     uint32_t w[4];
     float4 r4[2];
     half8_t bA[8], bB[8], a00, a01, a10, a11;
+    auto load_w = [&](const uint8_t *sb, int kk) __attribute__((always_inline)) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(sb + kXB + kk * kHW + wave * 1024 + lane * 16);
+        w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+    };
     // A fragments of half h (words 2h, 2h + 1) for column blocks 0 and 1
     auto make_a = [&](int h, half8_t &c0, half8_t &c1) __attribute__((always_inline)) {
         u32x4_t u0 = __builtin_bit_cast(u32x4_t, dequant_exact<4>(w, 2 * h, ec));
@@ -888,20 +940,10 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
         c0 = __builtin_bit_cast(half8_t, u0);
         c1 = __builtin_bit_cast(half8_t, u1);
     };
-    int pend_slot = 0, pend_kt = 0;
+    // MODE bit 8: the pending stage's pieces, issued between MFMA quarters of substeps 2 and 3
+    int pend_slot = 0, pend_st = 0;
     bool pend_gf = false, pend_on = false;
-    auto piece = [&](int p) __attribute__((always_inline)) {
-        if (!pend_on) return;
-        const uint32_t base = sbase + static_cast<uint32_t>(pend_slot * kHStage);
-        if (p < 4)
-            blds16_asm(xr, xo[p], static_cast<uint32_t>(pend_kt * kBK * 2),
-                       base + static_cast<uint32_t>(wave * 1024 + p * 0x2000));
-        else if (p == 4)
-            blds16_asm(wr, wo, static_cast<uint32_t>(pend_kt * 1024), base + static_cast<uint32_t>(kHX + wave * 1024));
-        else if (pend_gf && has_g)
-            blds16_asm(gr, wo, static_cast<uint32_t>((pend_kt >> 1) * Npad * 4),
-                       base + static_cast<uint32_t>(kHX + kHW + wave * 1024));
-    };
+    constexpr int kPPS = (L::kPieces + 1) / 2;   // pieces per late substep (3 / 4)
     auto mma = [&](int t, int cb, const half8_t &a, const half8_t &b) __attribute__((always_inline)) {
         acc[t][cb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, acc[t][cb], 0, 0, 0);
     };
@@ -914,26 +956,34 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
             acc[t][cb][3] *= r4[cb].w;
         }
     };
-    // Substep j: 16 MFMAs (token blocks 8 (j & 1) + i, both column blocks) of half j >> 1; the next
-    // substep's B fragments; substep 2 starts with the A fragments of half 1.
+    // Substep j: 16 MFMAs (8 token blocks x both column blocks); the next substep's B fragments and
+    // the A fragments it needs (TB = 16: half 1's at the start of substep 2, once half 0's are dead;
+    // TB = 8: the next substep's, built during this one).
     auto sub = [&](const uint8_t *sb, half8_t (&bc)[8], half8_t (&bn)[8], int j, bool gf) __attribute__((always_inline)) {
-        const int tb0 = 8 * (j & 1);
-        const half8_t &a0 = j < 2 ? a00 : a10;
-        const half8_t &a1 = j < 2 ? a01 : a11;
+        const int tb0 = sj_tb0(j);
+        const bool use1 = TB == 16 ? (j >= 2) : (j & 1);
+        const half8_t &a0 = use1 ? a10 : a00;
+        const half8_t &a1 = use1 ? a11 : a01;
         __builtin_amdgcn_sched_barrier(0);
-        if (j == 2) {   // half 1's A fragments once half 0's are dead (register budget)
+        if (TB == 16 && j == 2) {
             make_a(1, a10, a11);
             __builtin_amdgcn_sched_barrier(0);
         }
+        if (TB == 8 && j == 1) load_w(sb, 1);   // k-step 1's words (k-step 0's last use was in substep 0)
         __builtin_amdgcn_s_setprio(1);
+        if (TB == 8 && j < 3) {   // the next substep's A fragments beside this substep's MFMAs
+            if (j & 1) make_a(0, a00, a01);
+            else make_a(1, a10, a11);
+        }
         if ((MODE & 256) != 0 && j >= 2) {
             // quarters of 4 MFMAs (2 token blocks), each with 2 of the next substep's B reads, and a
             // DMA piece between quarters
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 if (j < 3) {
-                    bn[2 * q] = *reinterpret_cast<const half8_t *>(sb + soff[(j + 1) >> 1] + (8 * ((j + 1) & 1) + 2 * q) * 16 * kBK * 2);
-                    bn[2 * q + 1] = *reinterpret_cast<const half8_t *>(sb + soff[(j + 1) >> 1] + (8 * ((j + 1) & 1) + 2 * q + 1) * 16 * kBK * 2);
+                    const uint8_t *nb = sb + sj_kk(j + 1) * L::kXSub + soff[sj_h(j + 1)] + sj_tb0(j + 1) * 16 * kBK * 2;
+                    bn[2 * q] = *reinterpret_cast<const half8_t *>(nb + (2 * q) * 16 * kBK * 2);
+                    bn[2 * q + 1] = *reinterpret_cast<const half8_t *>(nb + (2 * q + 1) * 16 * kBK * 2);
                 }
                 mma(tb0 + 2 * q, 0, a0, bc[2 * q]);
                 mma(tb0 + 2 * q, 1, a1, bc[2 * q]);
@@ -946,7 +996,7 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
                 __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                 __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
                 __builtin_amdgcn_sched_barrier(0);
-                if (q < 3) piece(3 * (j - 2) + q);
+                if (pend_on && q < kPPS) piece(kPPS * (j - 2) + q, pend_slot, pend_st, pend_gf);
                 __builtin_amdgcn_sched_barrier(0);
             }
             __builtin_amdgcn_s_setprio(0);
@@ -954,7 +1004,7 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
             return;
         }
         if (j < 3) read_b(bn, sb, j + 1);
-        if (gf && j < 2) {
+        if (gf && (TB == 16 ? j < 2 : j == 0)) {
             // acc <- acc * r_g right before each token block's first MFMA of the group (block i + 1's
             // rescale beside block i's MFMAs)
 #pragma unroll
@@ -992,21 +1042,31 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
     };
-    const bool grp_b = STAG && wave >= 4;
-    auto step = [&](int slot, int kt, auto gf_tag) __attribute__((always_inline)) {
-        constexpr bool GF = decltype(gf_tag)::value;
-        const bool issue = kt + 2 < nk;
-        if (!STAG && issue) stage((slot + 2) % 3, kt + 2, GF);
-        const uint8_t *sb = smem + slot * kHStage;
-        {
-            const uint4 v = *reinterpret_cast<const uint4 *>(sb + kHX + wave * 1024 + lane * 16);
-            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+    // Waits until at most the pieces of one stage (the one issued in this stage's second half) are
+    // outstanding: 5 / 6 (TB = 16, + the group data) or 6 / 7 (TB = 8).
+    auto wait_one_stage = [&](bool gf) __attribute__((always_inline)) {
+        if constexpr (TB == 16) {
+            if (gf && has_g) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+        } else {
+            if (gf && has_g) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
         }
+    };
+    const bool grp_b = STAG && wave >= 4;
+    // One stage on ring slot `slot` (stage si); slot (si + 2) % 3 receives stage si + 2.  GF: the stage
+    // opens a group (every stage at TB = 8; TB = 16: even k-steps, so si + 2 opens one iff si does).
+    auto step = [&](int slot, int si, auto gf_tag) __attribute__((always_inline)) {
+        constexpr bool GF = decltype(gf_tag)::value;
+        const bool issue = si + 2 < ns;
+        if (!STAG && issue) stage((slot + 2) % 3, si + 2, GF);
+        const uint8_t *sb = smem + slot * kStage;
+        load_w(sb, 0);
         if constexpr (GF) {
             half2_t nz, sc;
-            split_sz(*reinterpret_cast<const uint32_t *>(sb + kHX + kHW + (wave * 32 + (lane & 31)) * 4), nz, sc);
+            split_sz(*reinterpret_cast<const uint32_t *>(sb + kXB + L::kWB + (wave * 32 + (lane & 31)) * 4), nz, sc);
             ec = exact_consts(nz);
-            const float *rl = reinterpret_cast<const float *>(sb + kHX + kHW + 1024) + wave * 32 + 4 * rq;
+            const float *rl = reinterpret_cast<const float *>(sb + kXB + L::kWB + 1024) + wave * 32 + 4 * rq;
             r4[0] = *reinterpret_cast<const float4 *>(rl);
             r4[1] = *reinterpret_cast<const float4 *>(rl + 16);
         }
@@ -1020,43 +1080,48 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
             if constexpr ((MODE & 256) != 0) {
                 pend_on = issue;
                 pend_slot = (slot + 2) % 3;
-                pend_kt = kt + 2;
+                pend_st = si + 2;
                 pend_gf = GF;
             } else if (issue) {
-                stage((slot + 2) % 3, kt + 2, GF);
+                stage((slot + 2) % 3, si + 2, GF);
             }
         }
         sub(sb, bA, bB, 2, GF);
         sub(sb, bB, bA, 3, GF);
         if (!grp_b) {
-            if (issue) {
-                if (GF && has_g) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-                else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
+            if (issue) wait_one_stage(GF);
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         barrier();
     };
 
     stage(0, 0, true);
-    stage(1, 1, false);
-    asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    stage(1, 1, TB == 8);
+    wait_one_stage(TB == 8);   // stage 0 landed (stage 1's pieces in flight)
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     if (grp_b) barrier();
     using GFt = std::integral_constant<bool, true>;
     using GFf = std::integral_constant<bool, false>;
-    for (int kt = 0; kt < nk; kt += 6) {
-        step(0, kt, GFt{});
-        step(1, kt + 1, GFf{});
-        if (kt + 2 < nk) {
-            step(2, kt + 2, GFt{});
-            step(0, kt + 3, GFf{});
+    if constexpr (TB == 16) {
+        // group = 2 k-steps, ring period 3: unroll 6 so each step's slot and group phase are static
+        for (int si = 0; si < ns; si += 6) {
+            step(0, si, GFt{});
+            step(1, si + 1, GFf{});
+            if (si + 2 < ns) {
+                step(2, si + 2, GFt{});
+                step(0, si + 3, GFf{});
+            }
+            if (si + 4 < ns) {
+                step(1, si + 4, GFt{});
+                step(2, si + 5, GFf{});
+            }
         }
-        if (kt + 4 < nk) {
-            step(1, kt + 4, GFt{});
-            step(2, kt + 5, GFf{});
+    } else {
+        for (int si = 0; si < ns; si += 3) {
+            step(0, si, GFt{});
+            if (si + 1 < ns) step(1, si + 1, GFt{});
+            if (si + 2 < ns) step(2, si + 2, GFt{});
         }
     }
     if (STAG && !grp_b) barrier();
@@ -1070,7 +1135,7 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
         const float4 s = *reinterpret_cast<const float4 *>(sl + 16 * cb);
         bv[cb] = *reinterpret_cast<const float4 *>(bias + nc0 + 16 * cb);
 #pragma unroll
-        for (int t = 0; t < 16; ++t) {
+        for (int t = 0; t < TB; ++t) {
             acc[t][cb][0] *= s.x;
             acc[t][cb][1] *= s.y;
             acc[t][cb][2] *= s.z;
@@ -1079,14 +1144,14 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
     }
     if constexpr ((MODE & 2) != 0) {   // lab ablation: keep the results live, store nothing
 #pragma unroll
-        for (int t = 0; t < 16; ++t)
+        for (int t = 0; t < TB; ++t)
 #pragma unroll
             for (int cb = 0; cb < 2; ++cb) asm volatile("" ::"v"(acc[t][cb]));
         return;
     }
     if constexpr (EPI == 1) {
 #pragma unroll
-        for (int t = 0; t < 16; ++t) {
+        for (int t = 0; t < TB; ++t) {
             const int m = m0 + 16 * t + row16;
             if (m >= M) continue;
 #pragma unroll
@@ -1098,16 +1163,16 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
         }
         return;
     }
-    const bool full = (m0 + 256 <= M) && (n0 + 256 <= N) && (N % 4) == 0;
+    const bool full = (m0 + 16 * TB <= M) && (n0 + 256 <= N) && (N % 4) == 0;
     if constexpr (std::is_same<YT, __half>::value) {
         if (full && (N % 8) == 0) {   // coalesced 16-B row stores through the drained ring
-            store_tile16_f16_lds(smem, acc, bv, Y, N, m0, n0, wave, lane);
+            store_tile16_f16_lds<TB>(smem, acc, bv, Y, N, m0, n0, wave, lane);
             return;
         }
     }
     if (full) {
 #pragma unroll
-        for (int t = 0; t < 16; ++t) {
+        for (int t = 0; t < TB; ++t) {
             YT *yrow = Y + static_cast<size_t>(m0 + 16 * t + row16) * N + nc0;
 #pragma unroll
             for (int cb = 0; cb < 2; ++cb)
@@ -1117,7 +1182,7 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
     } else {
         const bool vec_ok = (N % 4) == 0;
 #pragma unroll
-        for (int t = 0; t < 16; ++t) {
+        for (int t = 0; t < TB; ++t) {
             const int m = m0 + 16 * t + row16;
             if (m >= M) continue;
             YT *yrow = Y + static_cast<size_t>(m) * N;
@@ -1129,19 +1194,19 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
     }
 }
 
-template <int MODE>
+template <int MODE, int TB = 16>
 void launch_horner16_t(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
-    const int nbm = (a.M + 255) / 256, nbn = a.Npad / 256;
+    const int nbm = (a.M + 16 * TB - 1) / (16 * TB), nbn = a.Npad / 256;
     const unsigned nb = static_cast<unsigned>(nbm * nbn);
     const PSampleEpi ep = a.epi ? *a.epi : PSampleEpi{};
     if (a.epi)
-        wq_horner16_kernel<float, 1, MODE><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
+        wq_horner16_kernel<float, 1, MODE, TB><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
                                                                a.epi->x_prev, a.N, a.Npad, nbm, nbn, ep);
     else if (y_f32)
-        wq_horner16_kernel<float, 0, MODE><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
+        wq_horner16_kernel<float, 0, MODE, TB><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
                                                                static_cast<float *>(a.Y), a.N, a.Npad, nbm, nbn, ep);
     else
-        wq_horner16_kernel<__half, 0, MODE><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
+        wq_horner16_kernel<__half, 0, MODE, TB><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
                                                                 static_cast<__half *>(a.Y), a.N, a.Npad, nbm, nbn, ep);
 }
 
@@ -1178,6 +1243,13 @@ int launch_horner_kg2_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
     else
         wq_horner_kg2_kernel<__half, 0><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
                                                            static_cast<__half *>(a.Y), a.N, a.Npad, nbm, nbn, ep);
+    DLLM_LAUNCH_CHECK();
+    return DLLM_OK;
+}
+
+int launch_horner_rows_gemm(const HornerGemmArgs &a, int rows, int y_f32, hipStream_t st) {
+    if (rows != 128) return fail(DLLM_ERR_INVALID_PARAMS, "Horner tiles: 128 rows");
+    launch_horner16_t<1 | 256, 8>(a, y_f32, st);
     DLLM_LAUNCH_CHECK();
     return DLLM_OK;
 }

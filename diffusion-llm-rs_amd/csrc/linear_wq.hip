@@ -1948,6 +1948,24 @@ bool horner_ready(const dllm_linear *hc, int M, hipStream_t st) {
     return ensure_horner(hc, st);
 }
 
+// The Horner kernel on 128-token tiles (wq_horner16_kernel<..., TB = 8>, x 256 columns, 128-deep
+// stages), for grids where the 256 x 256 Horner grid leaves CUs idle but 128 x 256 tiles fill a round
+// (M = 2048 at N = 4096; the 2-GPU column shard, M = 4096 x N 2048).  Lab A/B only (variant 323):
+// against the fold form on those grids it measured -2.8 % on one box and +8 % on another (M = 2048:
+// 64.9 vs 66.7 us, 72.5 vs 67.0 us; profiles/r04_horner/), so the fold form stays the product path.
+// Returns the tile rows, 0 = not applicable.
+int horner_rows(const dllm_linear *hc, int M) {
+#if DLLM_LAB
+    const int np = static_cast<int>(hc->Npad);
+    if (hc->variant != 323 || !horner_shape(hc) || hc->hstate != 1) return 0;
+    if (((M + 127) / 128) * (np / 256) >= kCUs) return 128;
+#else
+    (void)hc;
+    (void)M;
+#endif
+    return 0;
+}
+
 // The KG2 Horner kernel (256 x 128 tiles, two k-groups): where neither the 256 x 256 Horner grid
 // nor the fold form's 128 x 256 grid fills a round but the 256 x 128 grid does (N = 4096: M
 // 1793..1920; measured at M = 1800: 69.2 vs 74.9 us).  At M = 2048 the 128 x 256 fold grid fills
@@ -2030,6 +2048,11 @@ int launch_prefill_auto(const dllm_linear *h, const __half *X, int M, YT *Y, hip
             const HornerGemmArgs a{X, M, (int)h->K, h->wdev, h->sz, h->hr, h->sf, h->bias, Y, (int)h->N,
                                    (int)h->Npad, epi};
             return launch_horner_kg2_gemm(a, std::is_same<YT, float>::value ? 1 : 0, st);
+        }
+        if (const int rows = BITS == 4 ? horner_rows(h, M) : 0) {
+            const HornerGemmArgs a{X, M, (int)h->K, h->wdev, h->sz, h->hr, h->sf, h->bias, Y, (int)h->N,
+                                   (int)h->Npad, epi};
+            return launch_horner_rows_gemm(a, rows, std::is_same<YT, float>::value ? 1 : 0, st);
         }
         ExactGemmArgs a = exact_args(h, X, M, Y, epi);
 #if DLLM_EXACT_HORNER   // A/B build: the 128 x 256 exact tiles in Horner form too
@@ -2444,8 +2467,8 @@ int dllm_linear_set_kernel_variant(dllm_linear_t h, int variant) {
         h->pplab = (variant - 100) % 32;
         return DLLM_OK;
     }
-    if (variant < -1 || (variant > 15 && (variant < 24 || variant > 31) && (variant < 300 || variant > 321 || variant == 313)))
-        return fail(DLLM_ERR_INVALID_PARAMS, "variant must be -1..15, 24..31, 300..312 or 314..321 (16..23, 32..95, 100..195, 200..263: ablations)");
+    if (variant < -1 || (variant > 15 && (variant < 24 || variant > 31) && (variant < 300 || variant > 323 || variant == 313)))
+        return fail(DLLM_ERR_INVALID_PARAMS, "variant must be -1..15, 24..31, 300..312 or 314..323 (16..23, 32..95, 100..195, 200..263: ablations)");
     h->variant = variant;
     h->dlab = h->rlab = h->pplab = h->dcfg = 0;
     return DLLM_OK;

@@ -15,6 +15,7 @@ import __graft_entry__ as g
 
 d = g.load_package(); import scripts._lab as _lab; _lab.select(d)
 M = N = K = int(os.environ.get("AB_K", "4096"))
+N = int(os.environ.get("AB_N", str(N)))
 M = int(os.environ.get("AB_M", str(M)))
 W = 0.02 * torch.randn(K, N, device="cuda")
 X = torch.randn(M, K, device="cuda").half()

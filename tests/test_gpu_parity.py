@@ -452,7 +452,8 @@ def test_linear_split_k_exact_integers(dllm, torch, orc):
 def test_linear_policy_exact_integers(dllm, torch, orc, precision, bits, M, N):
     """Every tile of both precision policies on exact-integer data (each group spans [0, 2^b - 1]:
     scale 1, zp 0; K = 768 = 6 groups, so every product and partial sum is an exact integer):
-    exact weights -- 128 x 256 tiles (M 4096 / 2048 at N 4096), the KG2 Horner tiles (int4, M 1800),
+    exact weights -- the Horner kernel (int4, M 4096 at N 4096), the 128 x 256 fold-form tiles (M 2048),
+    the KG2 Horner tiles (int4, M 1800),
     128 x 128 + group-aligned split-K
     (N 1024 / 512, M 512, 300), the exact decode kernel (M <= 64, one or 4 column tiles, K split) --
     and rounded weights (256 x 256, 256 x 128 two k-groups, 128 x 128 split-K, decode), with bias,
@@ -477,7 +478,7 @@ def test_linear_policy_exact_integers(dllm, torch, orc, precision, bits, M, N):
 
 
 @pytest.mark.parametrize("M,N,group", [(4096, 4096, 128), (2048, 4096, 128), (2048, 4096, 64), (2048, 4096, 256),
-                                       (4096, 1024, 128), (4096, 512, 128), (256, 4096, 128), (65, 4096, 256),
+                                       (4096, 2048, 128), (3001, 4096, 128), (4096, 1024, 128), (4096, 512, 128), (256, 4096, 128), (65, 4096, 256),
                                        (64, 4096, 128), (40, 1024, 64), (16, 4096, 128), (1, 4096, 256)])
 def test_linear_exact_weights_tight(dllm, torch, orc, M, N, group):
     """DLLM_PRECISION_EXACT: the MFMA consumes the exact integer (q - zp) and the f32 scale is
@@ -501,10 +502,12 @@ def test_linear_exact_weights_tight(dllm, torch, orc, M, N, group):
 
 
 @pytest.mark.parametrize("spread,M,K", [(8, 4096, 4096), (8, 8000, 1024), (8, 4300, 1024), (30, 4096, 2048), (45, 4096, 1024),
-                                         (8, 1800, 4096), (30, 1850, 2048), (45, 1800, 1024)])
+                                         (8, 1800, 4096), (30, 1850, 2048), (45, 1800, 1024),
+                                         (8, 2048, 4096), (30, 3000, 2048), (45, 2048, 1024)])
 def test_linear_horner_scale_spread(dllm, torch, orc, spread, M, K):
     """The 256 x 256-tile exact kernel (int4 g128, >= 256 tiles) keeps one accumulator in Horner form:
-    acc <- acc * (s_{g-1} / s_g) + T_g, times s_{G-1} at the end; at M = 1800 / 1850 (120 such tiles,
+    acc <- acc * (s_{g-1} / s_g) + T_g, times s_{G-1} at the end; at M = 2048 / 3000 the fold form
+    runs (the 256 x 256 grid leaves CUs idle); at M = 1800 / 1850 (120 such tiles,
     240 of the fold form's 128 x 256) the 256 x 128-tile KG2 kernel runs one chain per K-half (the
     second starting from a zero accumulator) and sums the two halves' partials times their last
     scales.  Per-(group, column) weight
