@@ -34,10 +34,11 @@ sys.path.insert(0, str(ROOT))
 PEAK_F16_TFLOPS = 2500.0   # MI355X dense f16/bf16 MFMA (MI355X_MICROARCH.md chip table)
 PEAK_HBM_GBS = 8000.0      # HBM3E spec
 # Revision tag of the default prefill GEMM kernel; a PMC record's traffic is quoted only when its
-# config carries the same tag (r04-horner16: wq_horner16_kernel of linear_horner.hip, the 256 x 256
-# Horner-form exact kernel on 16x16x32 MFMAs, stage DMA pieces spread between MFMA pairs, the
-# LDS-staged coalesced f16 store written with non-temporal 16-B stores).
-GEMM_REV = "r04-horner16"
+# config carries the same tag (r04-horner16b: wq_horner16_kernel of linear_horner.hip, the 256 x 256
+# Horner-form exact kernel on 16x16x32 MFMAs, conflict-free X swizzle, half 1's A fragments built
+# behind substep 1, stage DMA pieces spread between MFMA pairs, the LDS-staged coalesced f16 store
+# written with non-temporal 16-B stores).
+GEMM_REV = "r04-horner16b"
 
 
 def parse():

@@ -45,6 +45,13 @@
 #ifndef DLLM_EXACT_RING2
 #define DLLM_EXACT_RING2 0
 #endif
+// DLLM_EXACT_S16 = 1: the fold kernels on 16x16x32 MFMAs (A/B builds only).  Bit-exact on the policy
+// grid, but no faster on the box measured (M 2048 x 4096: 75.7 vs 77.4 us; the 4-GPU shard 4096 x 1024
+// 42.7 vs 42.0; 4096 x 512 26.7 vs 24.6; profiles/r04_shard/exact_s16_ab.jsonl), so the product keeps
+// the 32x32x16 form here (the Horner kernel's 16x16x32 form wins on 3 of 4 boxes).
+#ifndef DLLM_EXACT_S16
+#define DLLM_EXACT_S16 0
+#endif
 #ifndef DLLM_EXACT_KG2
 #define DLLM_EXACT_KG2 1
 #endif
@@ -57,6 +64,30 @@
 #include <algorithm>
 #include <type_traits>
 #include <utility>
+
+#ifndef DLLM_EXACT_MF16_ABL
+#define DLLM_EXACT_MF16_ABL 0
+#endif
+#if DLLM_EXACT_MF16_ABL
+// A/B build only (results wrong, timing only): each 32x32x16 MFMA replaced by two 16x16x32 MFMAs
+// on the same operands -- the MFMA shape's effect on the held clock (as lab ablation 319 did for
+// the Horner kernel).
+__device__ __forceinline__ float16_t exact_mf16_abl(const half8_t &a, const half8_t &b, float16_t c) {
+    typedef float fx4 __attribute__((ext_vector_type(4)));
+    typedef float fx8 __attribute__((ext_vector_type(8)));
+    fx4 c0 = __builtin_shufflevector(c, c, 0, 1, 2, 3), c1 = __builtin_shufflevector(c, c, 4, 5, 6, 7);
+    c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c1, 0, 0, 0);
+    const fx8 lo = __builtin_shufflevector(c0, c1, 0, 1, 2, 3, 4, 5, 6, 7);
+    const fx8 hi = __builtin_shufflevector(c, c, 8, 9, 10, 11, 12, 13, 14, 15);
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+}
+#define EXACT_MFMA(a, b, c) exact_mf16_abl((a), (b), (c))
+constexpr int kExactMF = 2;
+#else
+#define EXACT_MFMA(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_f16((a), (b), (c), 0, 0, 0)
+constexpr int kExactMF = 1;
+#endif
 
 namespace dllm {
 namespace {
@@ -90,8 +121,63 @@ struct ExactStage {
 // KG = 2: two k-groups of NW waves share the block's tile, k-group g taking the g-th half of the
 // slice's stages (own LDS stage parts, same barriers); their sums are added in the epilogue,
 // k-group 0's first: a tile-starved grid gets two waves per SIMD without a second launch.
+typedef float fx4e_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4e_t __attribute__((ext_vector_type(4)));
+
+// S16 accumulator element (t, cb, i) of a lane: token 16 t + (lane & 15), column 32 wave + 16 cb +
+// 4 (lane >> 4) + i.  The f16 tile (acc + b) through the drained ring as 16-B row chunks: rows of
+// 64 NW bytes, passes of as many whole 16-token blocks as fit.
+template <int NW, int MR>
+__device__ __forceinline__ void store_tile16x_f16_lds(uint8_t *img, int cap, const fx4e_t (&acc)[2 * MR][2],
+                                                      const float4 (&bv)[2], __half *Y, int N, int m0, int n0,
+                                                      int wave, int lane) {
+    constexpr int kRowB = 64 * NW, kCpr = 4 * NW, kRows = 32 * MR;
+    const int row16 = lane & 15, rq = lane >> 4;
+    const int per_pass = (cap / kRowB) >= kRows ? kRows : ((cap / kRowB) / 16) * 16;
+    for (int p0 = 0; p0 < kRows; p0 += per_pass) {
+#pragma unroll
+        for (int t = 0; t < 2 * MR; ++t) {
+            if (t * 16 < p0 || t * 16 >= p0 + per_pass) continue;
+            const int tr = t * 16 - p0 + row16;
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb) {
+                const int pc = (4 * wave + 2 * cb + (rq >> 1)) ^ (tr & (kCpr - 1));
+                union { __half h[4]; uint2 u; } pk;
+                pk.h[0] = __float2half_rn(acc[t][cb][0] + bv[cb].x);
+                pk.h[1] = __float2half_rn(acc[t][cb][1] + bv[cb].y);
+                pk.h[2] = __float2half_rn(acc[t][cb][2] + bv[cb].z);
+                pk.h[3] = __float2half_rn(acc[t][cb][3] + bv[cb].w);
+                *reinterpret_cast<uint2 *>(img + tr * kRowB + pc * 16 + (rq & 1) * 8) = pk.u;
+            }
+        }
+        __syncthreads();
+        constexpr int kRowsPerInst = 1024 / kRowB;
+        const int c = lane % kCpr;
+        const int nrows = per_pass < kRows - p0 ? per_pass : kRows - p0;
+        for (int t0 = wave * kRowsPerInst; t0 < nrows; t0 += NW * kRowsPerInst) {
+            const int t = t0 + lane / kCpr;
+            const uint4 v = *reinterpret_cast<const uint4 *>(img + t * kRowB + ((c ^ (t & (kCpr - 1))) * 16));
+#if DLLM_NT_STORE
+            typedef unsigned int u4nt __attribute__((ext_vector_type(4)));
+            __builtin_nontemporal_store(u4nt{v.x, v.y, v.z, v.w},
+                                        reinterpret_cast<u4nt *>(Y + static_cast<size_t>(m0 + p0 + t) * N + n0 + 8 * c));
+#else
+            *reinterpret_cast<uint4 *>(Y + static_cast<size_t>(m0 + p0 + t) * N + n0 + 8 * c) = v;
+#endif
+        }
+        __syncthreads();
+    }
+}
+
+// S16: the MFMAs are 16x16x32 (not TM / HORN).  The chip holds a higher clock on that shape at the
+// same FLOPs (MI355X_MICROARCH.md, DVFS give-back item 7); per wave the 32 columns x 32 MR tokens are
+// 2 column blocks x 2 MR token blocks of 16 x 16 (acc16 / tacc16: the same registers as acc / tacc).
+// A substep v (16 deep in the 32x32 form) becomes (32-deep half (v % 4) / 2, token blocks
+// MR (v % 2) ..): the same MFMA work, so the group / fold / ring logic is unchanged; the A fragments
+// of a half come from the same weight words through dequant_exact + v_permlane16_swap (as
+// wq_horner16_kernel), the X tile uses the conflict-free (row >> 1) & 5 chunk swizzle.
 template <int BITS, typename YT, int NW, int MR, int SPS, int KPG, bool SPLIT = false, int EPI = 0, bool TM = false,
-          int TMB = 1, bool WREG = false, int GPS = 1, int RING = 3, int KG = 1, bool HORN = false>
+          int TMB = 1, bool WREG = false, int GPS = 1, int RING = 3, int KG = 1, bool HORN = false, bool S16 = false>
 __global__ void __launch_bounds__(NW * KG * 64, NW * KG >= 8 ? 1 : 2)
 wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdev,
                      const uint32_t *__restrict__ sz, const float *__restrict__ sf, const float *__restrict__ bias,
@@ -105,6 +191,7 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
     static_assert(GPS == 1 || (KPG == 1 && !TM && (4 * SPS) % GPS == 0 && 2 * GPS <= NW), "whole groups per stage");
     static_assert(RING == 3 || (RING >= 2 && RING <= 8 && !TM), "ring depth");
     static_assert(KG == 1 || (!TM && RING * KG * SL::kBytes >= (KG - 1) * NW * 64 * MR * 16 * 4), "k-group combine fits the ring");
+    static_assert(!S16 || (!TM && !HORN), "16x16x32 form: fold kernels");
     constexpr int kBMt = 32 * MR, kBNt = 32 * NW;
     // RING stages of KG parts each (k-group g's part of stage i at ring + (i KG + g) kBytes)
     __shared__ __attribute__((aligned(16))) uint8_t ring[RING * KG * SL::kBytes];
@@ -144,7 +231,7 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
     for (int i = 0; i < SL::kR1; ++i) {
         const int row = (i * NW + wave) * 8 + (lane >> 3);
         const int rrow = (m0 + row < M ? m0 + row : M - 1) - m0;
-        const int c = chunk_st ^ ((row >> 1) & 7);
+        const int c = chunk_st ^ ((row >> 1) & (S16 ? 5 : 7));
         xoff[i] = static_cast<uint32_t>((rrow * K + c * 8) * 2);
     }
     const __amdgpu_buffer_rsrc_t xrs = raw_rsrc(X + static_cast<size_t>(m0) * K);
@@ -201,12 +288,23 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
         else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((RING - 2) * (SL::kXRounds + SL::kWOps)) : "memory");
     };
 
-    float16_t acc[MR], tacc[TM ? TMB : MR];
+    float16_t acc[S16 ? 1 : MR], tacc[TM ? TMB : (S16 ? 1 : MR)];
+    fx4e_t acc16[S16 ? 2 * MR : 1][2], tacc16[S16 ? 2 * MR : 1][2];
 #pragma unroll
-    for (int r = 0; r < MR; ++r)
+    for (int r = 0; r < (S16 ? 1 : MR); ++r)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[r][e] = 0.0f;
+#pragma unroll
+    for (int t = 0; t < (S16 ? 2 * MR : 1); ++t)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) acc16[t][cb] = fx4e_t{0.f, 0.f, 0.f, 0.f};
     const float16_t zero16 = {};
+    const fx4e_t zero4 = {0.f, 0.f, 0.f, 0.f};
+    const int row16 = lane & 15, rq = lane >> 4;
+    int soff16[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+        soff16[h] = row16 * (kBK * 2) + (((4 * h + (((rq & 1) << 1) | (rq >> 1))) ^ ((row16 >> 1) & 5)) << 4);
 
     const int hsel = lane >> 5;
     const int rowx = ((lane & 31) >> 1) & 7;
@@ -214,11 +312,32 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
 #pragma unroll
     for (int j = 0; j < 4; ++j) soff[j] = (lane & 31) * (kBK * 2) + ((((2 * j + hsel) ^ rowx)) << 4);
 
-    // B fragments of substep v (slab v / 4, 16-deep step v % 4) for the MR token reps.
+    // B fragments of substep v (slab v / 4, 16-deep step v % 4) for the MR token reps; S16: of the
+    // half (v % 4) / 2 for token blocks MR (v % 2) + r.
     auto read_b = [&](half8_t (&b)[MR], const uint8_t *sb, int v) __attribute__((always_inline)) {
 #pragma unroll
-        for (int r = 0; r < MR; ++r)
-            b[r] = *reinterpret_cast<const half8_t *>(sb + (v / 4) * SL::kX1 + soff[v % 4] + r * 32 * kBK * 2);
+        for (int r = 0; r < MR; ++r) {
+            if constexpr (S16)
+                b[r] = *reinterpret_cast<const half8_t *>(sb + (v / 4) * SL::kX1 + soff16[(v % 4) / 2] +
+                                                          (MR * (v % 2) + r) * 16 * kBK * 2);
+            else
+                b[r] = *reinterpret_cast<const half8_t *>(sb + (v / 4) * SL::kX1 + soff[v % 4] + r * 32 * kBK * 2);
+        }
+    };
+    // S16: the two 16x16x32 A fragments (column blocks 0, 1) of a 32-deep half from the words of the
+    // 32x32 layout (substeps 2h, 2h + 1)
+    auto make_a16 = [&](const uint32_t (&wb)[BITS], int h, const ExactConsts &e, half8_t &c0, half8_t &c1)
+        __attribute__((always_inline)) {
+        u32x4e_t u0 = __builtin_bit_cast(u32x4e_t, dequant_exact<BITS>(wb, 2 * h, e));
+        u32x4e_t u1 = __builtin_bit_cast(u32x4e_t, dequant_exact<BITS>(wb, 2 * h + 1, e));
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const auto r = __builtin_amdgcn_permlane16_swap(u0[q], u1[q], false, false);
+            u0[q] = r[0];
+            u1[q] = r[1];
+        }
+        c0 = __builtin_bit_cast(half8_t, u0);
+        c1 = __builtin_bit_cast(half8_t, u1);
     };
 
     // One stage (SPS slabs) on sb; stage pf receives stage kt + 2.  GF: first stage of a group (the
@@ -253,15 +372,24 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
         }
         half8_t bA[MR], bB[MR];
         read_b(bA, sb, 0);
-        half8_t aA = dequant_exact<BITS>(w[0], 0, ec[0]), aB;
+        half8_t aA, aB;
+        half8_t a16[2][2];   // S16: [half parity][column block]
+        if constexpr (S16) make_a16(w[0], 0, ec[0], a16[0][0], a16[0][1]);
+        else aA = dequant_exact<BITS>(w[0], 0, ec[0]);
         // Scales of a group (lane half hsel holds columns 4 hsel + 8 qd + (0..3) of the wave's 32): GPS = 1
         // reads them at the head of the stage so the fold never waits on LDS; GPS > 1 at the head of
         // each group's last substep.
         float4 s4[4];
         auto read_s4 = [&](int g) __attribute__((always_inline)) {
-            const float *sfl = reinterpret_cast<const float *>(sb + SL::kX + SL::kW + SL::kSZ + g * 1024) + wave * 32 + 4 * hsel;
+            if constexpr (S16) {   // column blocks 0, 1: columns 16 cb + 4 rq + (0..3)
+                const float *sfl = reinterpret_cast<const float *>(sb + SL::kX + SL::kW + SL::kSZ + g * 1024) + wave * 32 + 4 * rq;
+                s4[0] = *reinterpret_cast<const float4 *>(sfl);
+                s4[1] = *reinterpret_cast<const float4 *>(sfl + 16);
+            } else {
+                const float *sfl = reinterpret_cast<const float *>(sb + SL::kX + SL::kW + SL::kSZ + g * 1024) + wave * 32 + 4 * hsel;
 #pragma unroll
-            for (int qd = 0; qd < 4; ++qd) s4[qd] = *reinterpret_cast<const float4 *>(sfl + 8 * qd);
+                for (int qd = 0; qd < 4; ++qd) s4[qd] = *reinterpret_cast<const float4 *>(sfl + 8 * qd);
+            }
         };
         if constexpr (HORN ? GF : (GL && GPS == 1)) read_s4(0);
         // acc[r] += s (.) T_g[r]
@@ -273,6 +401,58 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
                 acc[r][4 * qd + 2] = __builtin_fmaf(s4[qd].z, tacc[r][4 * qd + 2], acc[r][4 * qd + 2]);
                 acc[r][4 * qd + 3] = __builtin_fmaf(s4[qd].w, tacc[r][4 * qd + 3], acc[r][4 * qd + 3]);
             }
+        };
+        // S16: fold token block t of both column blocks
+        auto fold16 = [&](int t) __attribute__((always_inline)) {
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb) {
+                acc16[t][cb][0] = __builtin_fmaf(s4[cb].x, tacc16[t][cb][0], acc16[t][cb][0]);
+                acc16[t][cb][1] = __builtin_fmaf(s4[cb].y, tacc16[t][cb][1], acc16[t][cb][1]);
+                acc16[t][cb][2] = __builtin_fmaf(s4[cb].z, tacc16[t][cb][2], acc16[t][cb][2]);
+                acc16[t][cb][3] = __builtin_fmaf(s4[cb].w, tacc16[t][cb][3], acc16[t][cb][3]);
+            }
+        };
+        // S16 substep v: 2 MR MFMAs (token blocks MR (v % 2) + r, both column blocks) of half (v % 4) / 2;
+        // a group's first touch of a token block starts from zero (substeps 0 and 1 of the group), its
+        // last (the group's last two substeps) folds it.  The next half's A fragments are built in the
+        // substep before it.
+        auto sub16 = [&](half8_t (&bc)[MR], half8_t (&bn)[MR], auto v_tag) __attribute__((always_inline)) {
+            constexpr int v = decltype(v_tag)::value;
+            constexpr int vg = GPS > 1 ? v % kSubG : v;   // substep within the group's stages
+            constexpr bool first = GPS > 1 ? vg < 2 : (GF && v < 2);
+            constexpr bool last = GPS > 1 ? vg >= kSubG - 2 : (GL && v >= kSub - 2);
+            constexpr int hp = (v / 2) % 2, tb0 = MR * (v % 2);
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (DLLM_EXACT_PRIO) __builtin_amdgcn_s_setprio(1);
+            if constexpr (GPS > 1 && vg == kSubG - 2) read_s4(v / kSubG);
+            if constexpr (v + 1 < kSub) read_b(bn, sb, v + 1);
+            if constexpr (v % 2 == 1 && v + 1 < kSub)
+                make_a16(w[(v + 1) / 4], ((v + 1) % 4) / 2, ec[(v + 1) / kSubG], a16[1 - hp][0], a16[1 - hp][1]);
+#pragma unroll
+            for (int r = 0; r < MR; ++r) {
+                tacc16[tb0 + r][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a16[hp][0], bc[r], first ? zero4 : tacc16[tb0 + r][0], 0, 0, 0);
+                tacc16[tb0 + r][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a16[hp][1], bc[r], first ? zero4 : tacc16[tb0 + r][1], 0, 0, 0);
+            }
+            if constexpr (last) {
+#pragma unroll
+                for (int r = 0; r < MR; ++r) fold16(tb0 + r);
+                __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);   // MFMAs of blocks 0, 1
+#pragma unroll
+                for (int i = 2; i < MR; ++i) {
+                    __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);   // fold of block i - 2
+                    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // MFMAs of block i
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < MR; ++i) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // MFMAs
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+                    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);   // VALU
+                }
+            }
+            if constexpr (DLLM_EXACT_PRIO) __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_sched_barrier(0);
         };
         auto sub = [&](half8_t (&bc)[MR], half8_t (&bn)[MR], const half8_t &ac, half8_t &an, auto v_tag) __attribute__((always_inline)) {
             constexpr int v = decltype(v_tag)::value;
@@ -290,13 +470,13 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
                 an = dequant_exact<BITS>(w[(v + 1) / 4], (v + 1) % 4, ec[(v + 1) / kSubG]);
 #pragma unroll
                 for (int r = 0; r < MR; ++r)
-                    tacc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bc[r], gfirst ? zero16 : tacc[r], 0, 0, 0);
+                    tacc[r] = EXACT_MFMA(ac, bc[r], gfirst ? zero16 : tacc[r]);
 #pragma unroll
                 for (int r = 0; r < MR; ++r) fold(r);
 #pragma unroll
                 for (int i = 0; i < MR; ++i) {
                     if (i >= 2) __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);   // fold of rep i - 2
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);               // MFMA rep i
+                    __builtin_amdgcn_sched_group_barrier(0x008, kExactMF, 0);               // MFMA rep i
                     __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);               // DS read
                     __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);               // dequant
                 }
@@ -314,23 +494,23 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
                             acc[r][4 * qd + 2] *= s4[qd].z;
                             acc[r][4 * qd + 3] *= s4[qd].w;
                         }
-                        acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bc[r], acc[r], 0, 0, 0);
+                        acc[r] = EXACT_MFMA(ac, bc[r], acc[r]);
                     }
                     __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
 #pragma unroll
                     for (int i = 0; i < MR; ++i) {
                         if (i + 1 < MR) __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);   // rescale of rep i + 1
-                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x008, kExactMF, 0);
                         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                         __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
                     }
                 } else {
 #pragma unroll
                     for (int r = 0; r < MR; ++r)
-                        acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bc[r], acc[r], 0, 0, 0);
+                        acc[r] = EXACT_MFMA(ac, bc[r], acc[r]);
 #pragma unroll
                     for (int i = 0; i < MR; ++i) {
-                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x008, kExactMF, 0);
                         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                         __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
                     }
@@ -338,16 +518,16 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
             } else if constexpr (HORN) {
 #pragma unroll
                 for (int r = 0; r < MR; ++r)
-                    acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bc[r], acc[r], 0, 0, 0);
+                    acc[r] = EXACT_MFMA(ac, bc[r], acc[r]);
             } else if constexpr (v + 1 < kSub) {
                 read_b(bn, sb, v + 1);
                 an = dequant_exact<BITS>(w[(v + 1) / 4], (v + 1) % 4, ec[(v + 1) / kSubG]);
 #pragma unroll
                 for (int r = 0; r < MR; ++r)
-                    tacc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bc[r], gfirst ? zero16 : tacc[r], 0, 0, 0);
+                    tacc[r] = EXACT_MFMA(ac, bc[r], gfirst ? zero16 : tacc[r]);
 #pragma unroll
                 for (int i = 0; i < MR; ++i) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+                    __builtin_amdgcn_sched_group_barrier(0x008, kExactMF, 0);   // MFMA
                     __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
                     __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);   // VALU
                 }
@@ -356,25 +536,32 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
                 // beside the group's own last MFMAs instead of after all of them.
 #pragma unroll
                 for (int r = 0; r < MR; ++r)
-                    tacc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bc[r], gfirst ? zero16 : tacc[r], 0, 0, 0);
+                    tacc[r] = EXACT_MFMA(ac, bc[r], gfirst ? zero16 : tacc[r]);
                 if constexpr (glast) {
 #pragma unroll
                     for (int r = 0; r < MR; ++r) fold(r);
-                    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // MFMA r = 0, 1
+                    __builtin_amdgcn_sched_group_barrier(0x008, 2 * kExactMF, 0);   // MFMA r = 0, 1
 #pragma unroll
                     for (int i = 2; i < MR; ++i) {
                         __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);  // fold of rep i - 2
-                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA rep i
+                        __builtin_amdgcn_sched_group_barrier(0x008, kExactMF, 0);   // MFMA rep i
                     }
                 }
             }
             if constexpr (DLLM_EXACT_PRIO) __builtin_amdgcn_s_setprio(0);
             __builtin_amdgcn_sched_barrier(0);
         };
-        [&]<int... Vs>(std::integer_sequence<int, Vs...>) __attribute__((always_inline)) {
-            ((Vs % 2 == 0 ? sub(bA, bB, aA, aB, std::integral_constant<int, Vs>{})
-                          : sub(bB, bA, aB, aA, std::integral_constant<int, Vs>{})), ...);
-        }(std::make_integer_sequence<int, kSub>{});
+        if constexpr (S16) {
+            [&]<int... Vs>(std::integer_sequence<int, Vs...>) __attribute__((always_inline)) {
+                ((Vs % 2 == 0 ? sub16(bA, bB, std::integral_constant<int, Vs>{})
+                              : sub16(bB, bA, std::integral_constant<int, Vs>{})), ...);
+            }(std::make_integer_sequence<int, kSub>{});
+        } else {
+            [&]<int... Vs>(std::integer_sequence<int, Vs...>) __attribute__((always_inline)) {
+                ((Vs % 2 == 0 ? sub(bA, bB, aA, aB, std::integral_constant<int, Vs>{})
+                              : sub(bB, bA, aB, aA, std::integral_constant<int, Vs>{})), ...);
+            }(std::make_integer_sequence<int, kSub>{});
+        }
         // Stage kt+1 must have landed; (RING 3) kt+2's DMAs may stay in flight across the barrier.
         if (issue) wait_prev();
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -415,7 +602,7 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
             // MFMA j of rep r reads bq[j]; the next rep's fragment j refills it right after.
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                tacc[r % TMB] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[j], bq[j], j == 0 ? zero16 : tacc[r % TMB], 0, 0, 0);
+                tacc[r % TMB] = EXACT_MFMA(a[j], bq[j], j == 0 ? zero16 : tacc[r % TMB]);
                 if (r + 1 < MR) bq[j] = *reinterpret_cast<const half8_t *>(sb + soff[j] + (r + 1) * 32 * kBK * 2);
             }
             if constexpr (TMB == 1) {
@@ -428,7 +615,7 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
             }
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x008, kExactMF, 0);   // MFMA
                 __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
                 __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);   // VALU (the previous rep's fold)
             }
@@ -492,7 +679,29 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
             }
         }
     }
-    if constexpr (KG >= 2) {
+    if constexpr (KG >= 2 && S16) {
+        constexpr int kXg = NW * MR * 4 * 64;   // float4s per k-group (4 MR per lane, as below)
+        float4 *xch = reinterpret_cast<float4 *>(ring) + (wave * MR * 4) * 64 + lane;
+        if (kg >= 1) {
+#pragma unroll
+            for (int t = 0; t < 2 * MR; ++t)
+#pragma unroll
+                for (int cb = 0; cb < 2; ++cb)
+                    xch[(kg - 1) * kXg + (t * 2 + cb) * 64] =
+                        make_float4(acc16[t][cb][0], acc16[t][cb][1], acc16[t][cb][2], acc16[t][cb][3]);
+        }
+        __syncthreads();
+        if (kg >= 1) return;
+#pragma unroll
+        for (int g = 1; g < KG; ++g)
+#pragma unroll
+            for (int t = 0; t < 2 * MR; ++t)
+#pragma unroll
+                for (int cb = 0; cb < 2; ++cb) {
+                    const float4 o = xch[(g - 1) * kXg + (t * 2 + cb) * 64];
+                    acc16[t][cb][0] += o.x; acc16[t][cb][1] += o.y; acc16[t][cb][2] += o.z; acc16[t][cb][3] += o.w;
+                }
+    } else if constexpr (KG >= 2) {
         // k-groups 1 .. KG-1 hand their sums to k-group 0 through the (drained) ring, 16 B per lane
         // per store; k-group 0 adds them in k-group order.
         constexpr int kXg = NW * MR * 4 * 64;   // float4s per k-group
@@ -517,72 +726,133 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
                     acc[r][4 * qd] += o.x; acc[r][4 * qd + 1] += o.y; acc[r][4 * qd + 2] += o.z; acc[r][4 * qd + 3] += o.w;
                 }
     }
-    // Epilogue: acc[r] reg e -> n = n0 + 32 wave + 4 hsel + 8 (e >> 2) + (e & 3), m = m0 + 32 r + (lane & 31).
-    const int nb0 = n0 + wave * 32 + 4 * hsel;
-    if constexpr (SPLIT) {
-        float *slab = ws + static_cast<size_t>(ks) * M * Npad;
+    if constexpr (S16) {
+        // element (t, cb, i): m = m0 + 16 t + (lane & 15), n = n0 + 32 wave + 16 cb + 4 rq + i
+        const int nc0 = n0 + wave * 32 + 4 * rq;
+        if constexpr (SPLIT) {
+            float *slab = ws + static_cast<size_t>(ks) * M * Npad;
 #pragma unroll
-        for (int r = 0; r < MR; ++r) {
-            const int m = m0 + r * 32 + (lane & 31);
-            if (m >= M) continue;
-            float *prow = slab + static_cast<size_t>(m) * Npad + nb0;
+            for (int t = 0; t < 2 * MR; ++t) {
+                const int m = m0 + 16 * t + row16;
+                if (m >= M) continue;
+                float *prow = slab + static_cast<size_t>(m) * Npad + nc0;
 #pragma unroll
-            for (int qd = 0; qd < 4; ++qd)
-                *reinterpret_cast<float4 *>(prow + 8 * qd) =
-                    make_float4(acc[r][4 * qd + 0], acc[r][4 * qd + 1], acc[r][4 * qd + 2], acc[r][4 * qd + 3]);
-        }
-        return;
-    }
-    float4 bv[4];
-#pragma unroll
-    for (int qd = 0; qd < 4; ++qd) bv[qd] = *reinterpret_cast<const float4 *>(bias + nb0 + 8 * qd);
-    if constexpr (EPI == 1) {
-#pragma unroll
-        for (int r = 0; r < MR; ++r) {
-            const int m = m0 + r * 32 + (lane & 31);
-            if (m >= M) continue;
-#pragma unroll
-            for (int qd = 0; qd < 4; ++qd) {
-                if (nb0 + 8 * qd >= N) continue;
-                psample4(epi, m, nb0 + 8 * qd, N, acc[r][4 * qd + 0] + bv[qd].x, acc[r][4 * qd + 1] + bv[qd].y,
-                         acc[r][4 * qd + 2] + bv[qd].z, acc[r][4 * qd + 3] + bv[qd].w);
+                for (int cb = 0; cb < 2; ++cb)
+                    *reinterpret_cast<float4 *>(prow + 16 * cb) =
+                        make_float4(acc16[t][cb][0], acc16[t][cb][1], acc16[t][cb][2], acc16[t][cb][3]);
             }
-        }
-        return;
-    }
-    const bool full = (m0 + kBMt <= M) && (n0 + kBNt <= N) && (N % 4) == 0;
-    if constexpr (std::is_same<YT, __half>::value && KG == 1 && NW * 64 >= 256) {
-        if (full && (N % 8) == 0) {   // coalesced 16-B row stores (16-B aligned rows) through the drained ring
-            store_tile_f16_lds<NW, MR>(ring, static_cast<int>(sizeof(ring)), acc, bv, Y, N, m0, n0, wave, lane);
             return;
         }
-    }
-    if (full) {
+        float4 bv16[2];
 #pragma unroll
-        for (int r = 0; r < MR; ++r) {
-            YT *yrow = Y + static_cast<size_t>(m0 + r * 32 + (lane & 31)) * N + nb0;
+        for (int cb = 0; cb < 2; ++cb) bv16[cb] = *reinterpret_cast<const float4 *>(bias + nc0 + 16 * cb);
+        if constexpr (EPI == 1) {
 #pragma unroll
-            for (int qd = 0; qd < 4; ++qd)
-                store4<YT>(yrow + 8 * qd, acc[r][4 * qd + 0] + bv[qd].x, acc[r][4 * qd + 1] + bv[qd].y,
-                           acc[r][4 * qd + 2] + bv[qd].z, acc[r][4 * qd + 3] + bv[qd].w);
+            for (int t = 0; t < 2 * MR; ++t) {
+                const int m = m0 + 16 * t + row16;
+                if (m >= M) continue;
+#pragma unroll
+                for (int cb = 0; cb < 2; ++cb) {
+                    if (nc0 + 16 * cb >= N) continue;
+                    psample4(epi, m, nc0 + 16 * cb, N, acc16[t][cb][0] + bv16[cb].x, acc16[t][cb][1] + bv16[cb].y,
+                             acc16[t][cb][2] + bv16[cb].z, acc16[t][cb][3] + bv16[cb].w);
+                }
+            }
+            return;
         }
-    } else {
+        const bool full16 = (m0 + kBMt <= M) && (n0 + kBNt <= N) && (N % 4) == 0;
+        if constexpr (std::is_same<YT, __half>::value && KG == 1 && NW * 64 >= 256) {
+            if (full16 && (N % 8) == 0) {
+                store_tile16x_f16_lds<NW, MR>(ring, static_cast<int>(sizeof(ring)), acc16, bv16, Y, N, m0, n0, wave, lane);
+                return;
+            }
+        }
         const bool vec_ok = (N % 4) == 0;
 #pragma unroll
-        for (int r = 0; r < MR; ++r) {
-            const int m = m0 + r * 32 + (lane & 31);
+        for (int t = 0; t < 2 * MR; ++t) {
+            const int m = m0 + 16 * t + row16;
             if (m >= M) continue;
             YT *yrow = Y + static_cast<size_t>(m) * N;
 #pragma unroll
-            for (int qd = 0; qd < 4; ++qd)
-                store_out4<YT>(yrow, bias, nb0 + 8 * qd, N, vec_ok, acc[r][4 * qd + 0], acc[r][4 * qd + 1],
-                               acc[r][4 * qd + 2], acc[r][4 * qd + 3]);
+            for (int cb = 0; cb < 2; ++cb) {
+                if (full16)
+                    store4<YT>(yrow + nc0 + 16 * cb, acc16[t][cb][0] + bv16[cb].x, acc16[t][cb][1] + bv16[cb].y,
+                               acc16[t][cb][2] + bv16[cb].z, acc16[t][cb][3] + bv16[cb].w);
+                else
+                    store_out4<YT>(yrow, bias, nc0 + 16 * cb, N, vec_ok, acc16[t][cb][0], acc16[t][cb][1],
+                                   acc16[t][cb][2], acc16[t][cb][3]);
+            }
+        }
+        return;
+    } else {
+        // Epilogue: acc[r] reg e -> n = n0 + 32 wave + 4 hsel + 8 (e >> 2) + (e & 3), m = m0 + 32 r + (lane & 31).
+        const int nb0 = n0 + wave * 32 + 4 * hsel;
+        if constexpr (SPLIT) {
+            float *slab = ws + static_cast<size_t>(ks) * M * Npad;
+    #pragma unroll
+            for (int r = 0; r < MR; ++r) {
+                const int m = m0 + r * 32 + (lane & 31);
+                if (m >= M) continue;
+                float *prow = slab + static_cast<size_t>(m) * Npad + nb0;
+    #pragma unroll
+                for (int qd = 0; qd < 4; ++qd)
+                    *reinterpret_cast<float4 *>(prow + 8 * qd) =
+                        make_float4(acc[r][4 * qd + 0], acc[r][4 * qd + 1], acc[r][4 * qd + 2], acc[r][4 * qd + 3]);
+            }
+            return;
+        }
+        float4 bv[4];
+    #pragma unroll
+        for (int qd = 0; qd < 4; ++qd) bv[qd] = *reinterpret_cast<const float4 *>(bias + nb0 + 8 * qd);
+        if constexpr (EPI == 1) {
+    #pragma unroll
+            for (int r = 0; r < MR; ++r) {
+                const int m = m0 + r * 32 + (lane & 31);
+                if (m >= M) continue;
+    #pragma unroll
+                for (int qd = 0; qd < 4; ++qd) {
+                    if (nb0 + 8 * qd >= N) continue;
+                    psample4(epi, m, nb0 + 8 * qd, N, acc[r][4 * qd + 0] + bv[qd].x, acc[r][4 * qd + 1] + bv[qd].y,
+                             acc[r][4 * qd + 2] + bv[qd].z, acc[r][4 * qd + 3] + bv[qd].w);
+                }
+            }
+            return;
+        }
+        const bool full = (m0 + kBMt <= M) && (n0 + kBNt <= N) && (N % 4) == 0;
+        if constexpr (std::is_same<YT, __half>::value && KG == 1 && NW * 64 >= 256) {
+            if (full && (N % 8) == 0) {   // coalesced 16-B row stores (16-B aligned rows) through the drained ring
+                store_tile_f16_lds<NW, MR>(ring, static_cast<int>(sizeof(ring)), acc, bv, Y, N, m0, n0, wave, lane);
+                return;
+            }
+        }
+        if (full) {
+    #pragma unroll
+            for (int r = 0; r < MR; ++r) {
+                YT *yrow = Y + static_cast<size_t>(m0 + r * 32 + (lane & 31)) * N + nb0;
+    #pragma unroll
+                for (int qd = 0; qd < 4; ++qd)
+                    store4<YT>(yrow + 8 * qd, acc[r][4 * qd + 0] + bv[qd].x, acc[r][4 * qd + 1] + bv[qd].y,
+                               acc[r][4 * qd + 2] + bv[qd].z, acc[r][4 * qd + 3] + bv[qd].w);
+            }
+        } else {
+            const bool vec_ok = (N % 4) == 0;
+    #pragma unroll
+            for (int r = 0; r < MR; ++r) {
+                const int m = m0 + r * 32 + (lane & 31);
+                if (m >= M) continue;
+                YT *yrow = Y + static_cast<size_t>(m) * N;
+    #pragma unroll
+                for (int qd = 0; qd < 4; ++qd)
+                    store_out4<YT>(yrow, bias, nb0 + 8 * qd, N, vec_ok, acc[r][4 * qd + 0], acc[r][4 * qd + 1],
+                                   acc[r][4 * qd + 2], acc[r][4 * qd + 3]);
+            }
         }
     }
 }
 
 template <int BITS, typename YT, int NW, int MR, int SPS, int KPG, int EPI, bool TM = false, int GPS = 1, int RING = 3,
-          int KG = 1, bool WREG = (DLLM_EXACT_WREG != 0 && BITS == 4 && !TM), bool HORN = false>
+          int KG = 1, bool WREG = (DLLM_EXACT_WREG != 0 && BITS == 4 && !TM), bool HORN = false,
+          bool S16 = (DLLM_EXACT_S16 != 0 && !TM && !HORN)>
 int launch_exact_tile(const ExactGemmArgs &a, int nsplit, hipStream_t st) {
     if constexpr (HORN) {
         const int nbm = (a.M + 32 * MR - 1) / (32 * MR), nbn = a.Npad / (32 * NW);
@@ -599,14 +869,14 @@ int launch_exact_tile(const ExactGemmArgs &a, int nsplit, hipStream_t st) {
     const PSampleEpi ep = a.epi ? *a.epi : PSampleEpi{};
     YT *Y = static_cast<YT *>(a.Y);
     if (nsplit == 1) {
-        wq_gemm_exact_kernel<BITS, YT, NW, MR, SPS, KPG, false, EPI, TM, 1, WREG, GPS, RING, KG><<<nb, NW * KG * 64, 0, st>>>(
+        wq_gemm_exact_kernel<BITS, YT, NW, MR, SPS, KPG, false, EPI, TM, 1, WREG, GPS, RING, KG, false, S16><<<nb, NW * KG * 64, 0, st>>>(
             a.X, a.M, a.K, a.wdev, a.sz, a.sf, a.bias, Y, a.N, a.Npad, a.group, nbm, nbn, 1, nullptr, ep);
         DLLM_LAUNCH_CHECK();
         return DLLM_OK;
     }
     float *ws = device_workspace(st, static_cast<size_t>(nsplit) * a.M * a.Npad * sizeof(float));
     if (!ws) return DLLM_ERR_HIP;
-    wq_gemm_exact_kernel<BITS, YT, NW, MR, SPS, KPG, true, 0, TM, 1, WREG, GPS, RING, KG><<<nb, NW * KG * 64, 0, st>>>(
+    wq_gemm_exact_kernel<BITS, YT, NW, MR, SPS, KPG, true, 0, TM, 1, WREG, GPS, RING, KG, false, S16><<<nb, NW * KG * 64, 0, st>>>(
         a.X, a.M, a.K, a.wdev, a.sz, a.sf, a.bias, Y, a.N, a.Npad, a.group, nbm, nbn, nsplit, ws);
     DLLM_LAUNCH_CHECK();
     const size_t q = static_cast<size_t>(a.M) * (a.Npad / 4);

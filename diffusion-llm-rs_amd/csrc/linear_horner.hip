@@ -71,6 +71,9 @@ __device__ __forceinline__ void horner_burst(__amdgpu_buffer_rsrc_t xr, uint32_t
         : "memory");
 }
 
+// (wq_horner16_kernel: MODE bit 10 = half 1's A fragments built right after substep 1 (product);
+// bit 11 = a non-group-first step's words and half-0 A fragments built at the end of the step
+// before (lab A/B 325, not adopted).)
 // MODE bit 0: the staggered schedule (product).  Lab ablations only (results wrong, timing only):
 // bit 1 no output stores; bit 2 no Horner rescale; bit 3 one dequant per k-step instead of four;
 // bit 4 one B fragment read per k-step instead of four; bit 5 no X DMA (weight words only); bit 6
@@ -854,7 +857,7 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
     for (int i = 0; i < L::kNX; ++i) {
         const int row = (i * 8 + wave) * 8 + (lane >> 3);
         const int rrow = (m0 + row < M ? m0 + row : M - 1) - m0;
-        const int c = (lane & 7) ^ ((row >> 1) & 7);
+        const int c = (lane & 7) ^ ((row >> 1) & 5);   // X chunk swizzle: see soff below
         xo[i] = static_cast<uint32_t>((rrow * K + c * 8) * 2);
     }
     const __amdgpu_buffer_rsrc_t xr = raw_rsrc(X + static_cast<size_t>(m0) * K);
@@ -903,9 +906,13 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
 
     const int row16 = lane & 15, rq = lane >> 4;
     const int cq = ((rq & 1) << 1) | (rq >> 1);   // k-chunk of lane row rq after the swap: 0, 2, 1, 3
+    // LDS slot of chunk g in row r: g ^ ((r >> 1) & 5).  With the lane rows' chunks 4h + {0, 2, 1, 3}
+    // this makes each ds_read_b128 lane group (16 lanes: 8 rows of one lane row, 8 of another whose
+    // chunk differs by 2) hit 16 distinct 16-B bank slots; the (r >> 1) & 7 swizzle of the 32x32
+    // kernel maps them 2-way onto 8.
     int soff[2];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) soff[h] = row16 * (kBK * 2) + (((4 * h + cq) ^ ((row16 >> 1) & 7)) << 4);
+    for (int h = 0; h < 2; ++h) soff[h] = row16 * (kBK * 2) + (((4 * h + cq) ^ ((row16 >> 1) & 5)) << 4);
 
     // substep j -> (k-step kk of the stage, half h, first token block tb0)
     auto sj_kk = [](int j) { return TB == 16 ? 0 : (j >> 1); };
@@ -957,15 +964,15 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
         }
     };
     // Substep j: 16 MFMAs (8 token blocks x both column blocks); the next substep's B fragments and
-    // the A fragments it needs (TB = 16: half 1's at the start of substep 2, once half 0's are dead;
-    // TB = 8: the next substep's, built during this one).
+    // the A fragments it needs (TB = 16: half 1's after substep 1, see step; TB = 8: the next
+    // substep's, built during this one).
     auto sub = [&](const uint8_t *sb, half8_t (&bc)[8], half8_t (&bn)[8], int j, bool gf) __attribute__((always_inline)) {
         const int tb0 = sj_tb0(j);
         const bool use1 = TB == 16 ? (j >= 2) : (j & 1);
         const half8_t &a0 = use1 ? a10 : a00;
         const half8_t &a1 = use1 ? a11 : a01;
         __builtin_amdgcn_sched_barrier(0);
-        if (TB == 16 && j == 2) {
+        if ((MODE & 1024) == 0 && TB == 16 && j == 2) {   // lab A/B: half 1's A fragments at substep 2
             make_a(1, a10, a11);
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -1061,7 +1068,11 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
         const bool issue = si + 2 < ns;
         if (!STAG && issue) stage((slot + 2) % 3, si + 2, GF);
         const uint8_t *sb = smem + slot * kStage;
-        load_w(sb, 0);
+        // MODE bit 11 (TB = 16): a non-group-first step's words and half-0 A fragments were built at
+        // the end of the step before (the wave's own weight-word DMA is complete after its vmcnt
+        // wait; the zero points are the group's), so they overlap that step's MFMA drain
+        constexpr bool kEarly = (MODE & 2048) != 0 && TB == 16;
+        if (!(kEarly && !GF)) load_w(sb, 0);
         if constexpr (GF) {
             half2_t nz, sc;
             split_sz(*reinterpret_cast<const uint32_t *>(sb + kXB + L::kWB + (wave * 32 + (lane & 31)) * 4), nz, sc);
@@ -1071,9 +1082,15 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
             r4[1] = *reinterpret_cast<const float4 *>(rl + 16);
         }
         read_b(bA, sb, 0);
-        make_a(0, a00, a01);
+        if (!(kEarly && !GF)) make_a(0, a00, a01);
         sub(sb, bA, bB, 0, GF);
         sub(sb, bB, bA, 1, GF);
+        if constexpr (TB == 16 && (MODE & 1024) != 0) {
+            // half 1's A fragments right behind substep 1's MFMAs (their registers free once those
+            // issue): the dequant runs while the MFMAs drain and the wave reaches the barrier
+            make_a(1, a10, a11);
+            __builtin_amdgcn_sched_barrier(0);
+        }
         if constexpr (STAG) {
             if (grp_b) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             barrier();
@@ -1091,6 +1108,12 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
         if (!grp_b) {
             if (issue) wait_one_stage(GF);
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        if constexpr (kEarly && GF) {   // the next (same-group) step's words and half-0 A fragments
+            __builtin_amdgcn_sched_barrier(0);
+            load_w(smem + ((slot + 1) % 3) * kStage, 0);
+            make_a(0, a00, a01);
+            __builtin_amdgcn_sched_barrier(0);
         }
         barrier();
     };
@@ -1256,6 +1279,17 @@ int launch_horner_rows_gemm(const HornerGemmArgs &a, int rows, int y_f32, hipStr
 
 int launch_horner_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
 #if DLLM_LAB
+    if (a.lab == 25) {   // lab A/B: the 16x16x32 kernel with MODE bit 11 (2 % slower on one box:
+                         // profiles/r04_horner/h16_early_dequant_ab.json)
+        launch_horner16_t<1 | 256 | 1024 | 2048>(a, y_f32, st);
+        DLLM_LAUNCH_CHECK();
+        return DLLM_OK;
+    }
+    if (a.lab == 24) {   // lab A/B: the 16x16x32 kernel with half 1's A fragments built at substep 2
+        launch_horner16_t<1 | 256>(a, y_f32, st);
+        DLLM_LAUNCH_CHECK();
+        return DLLM_OK;
+    }
     if (a.lab == 21) {   // lab A/B: the round-3 MFMA shape (32x32x16) with the product schedule
         launch_horner_t<1 | 256>(a, y_f32, st);
         DLLM_LAUNCH_CHECK();
@@ -1305,7 +1339,7 @@ int launch_horner_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
         return DLLM_OK;
     }
 #endif
-    launch_horner16_t<1 | 256>(a, y_f32, st);
+    launch_horner16_t<1 | 256 | 1024>(a, y_f32, st);
     DLLM_LAUNCH_CHECK();
     return DLLM_OK;
 }

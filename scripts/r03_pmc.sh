@@ -17,4 +17,4 @@ for C in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_I
   rc=$?; echo "pass $i rc=$rc"
   [ $rc -eq 0 ] || exit $rc
 done
-python3 scripts/pmc_to_json.py "$OUT" "$OUT/pmc_gemm.json" "$KRE" 4096 4096 4096 4 128 "${GEMM_REV:-r04-horner16}"
+python3 scripts/pmc_to_json.py "$OUT" "$OUT/pmc_gemm.json" "$KRE" 4096 4096 4096 4 128 "${GEMM_REV:-r04-horner16b}"

@@ -38,11 +38,11 @@ for s in ${STEPS:-tests chain quant horner shard}; do
              LIBS=diffusion-llm-rs_amd/lib/libdllm_hip.so ROUNDS=1 SHAPES=${CSHAPES:-4096:1024,4096:512,4096:4096} step clkshard_$i 120 rocprofv3 --pmc $C --kernel-include-regex "wq_gemm_exact|wq_horner" -d $O/clkshard_$i -o pmc --output-format csv -- python scripts/gemm_ab.py
            done;;
     shape) step shape 200 python scripts/horner_ab.py -1 319 314 320;;
-    h128) AB_M=2048 step h128 200 python scripts/horner_ab.py -1 322 -1 322
-          AB_M=3000 step h128_3000 120 python scripts/horner_ab.py -1 322
-          AB_M=4096 AB_N=2048 step h128_shard2 120 python scripts/horner_ab.py -1 322
+    h128) AB_M=2048 step h128 200 python scripts/horner_ab.py -1 323 -1 323
+          AB_M=3000 step h128_3000 120 python scripts/horner_ab.py -1 323
+          AB_M=4096 AB_N=2048 step h128_shard2 120 python scripts/horner_ab.py -1 323
 ;;
-    h16) step h16 200 python scripts/horner_ab.py -1 321 -1 321;;
+    h16) step h16 200 python scripts/horner_ab.py -1 325 321 -1 325 321;;
     blas) step blas 120 python scripts/blas_shapes.py
           LIBS=diffusion-llm-rs_amd/lib/libdllm_hip.so ROUNDS=2 step shard_ab 200 python scripts/gemm_ab.py;;
     tp) DLLM_BENCH_BACKEND=gloo step tp_trace 400 rocprofv3 --kernel-trace -d $O/tp -o kt --output-format csv -- python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --tp-steps 4 --no-cpu;;
