@@ -202,3 +202,18 @@ def test_sharded_kv_state_bitexact(loop_results, unsharded):
                                           np.array([s, z], np.float32).view(np.uint32)), (i, tag, which)
     assert n_full % WORLD == 0
     assert widths[: STEPS // 2 - 1] == [4] * (STEPS // 2 - 1) and widths[-1] == 0, widths
+
+
+def test_cpu_sample_is_the_step_sequence(unsharded):
+    """``DenoiseLoop.sample`` on the CPU (device='cpu' forces the serial schedule and touches no CUDA
+    stream) returns the state of the step-by-step loop above, bit for bit."""
+    import __graft_entry__ as g
+    d = g.load_package()
+    xs, _ = unsharded
+    Ws, bs, K, V, x0 = _inputs()
+    layers = [OracleLinear(torch.from_numpy(W), torch.from_numpy(b) if j % 2 else None, 4, 128)
+              for j, (W, b) in enumerate(zip(Ws, bs))]
+    loop = d.DenoiseLoop(layers, _cfg(d), cumprod=d.Cumprod.INCLUSIVE, seed=SEED, kv_cache=None, ops=OracleLoopOps,
+                         device="cpu")
+    out = loop.sample(torch.from_numpy(x0), STEPS)
+    assert np.array_equal(out.numpy(), xs[STEPS])
