@@ -40,6 +40,27 @@ typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
 typedef float float16_t __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
+#ifndef DLLM_ATTN_MF16_ABL
+#define DLLM_ATTN_MF16_ABL 0
+#endif
+#if DLLM_ATTN_MF16_ABL
+// A/B build only (results wrong, timing only): kv_attention5's 32x32x16 MFMAs each replaced by two
+// 16x16x32 on the same operands -- the MFMA shape's effect on the held clock.
+__device__ __forceinline__ float16_t attn_mf16_abl(const half8_t &a, const half8_t &b, float16_t c) {
+    typedef float fx4 __attribute__((ext_vector_type(4)));
+    typedef float fx8 __attribute__((ext_vector_type(8)));
+    fx4 c0 = __builtin_shufflevector(c, c, 0, 1, 2, 3), c1 = __builtin_shufflevector(c, c, 4, 5, 6, 7);
+    c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c1, 0, 0, 0);
+    const fx8 lo = __builtin_shufflevector(c0, c1, 0, 1, 2, 3, 4, 5, 6, 7);
+    const fx8 hi = __builtin_shufflevector(c, c, 8, 9, 10, 11, 12, 13, 14, 15);
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+}
+#define ATTN5_MFMA(a, b, c) attn_mf16_abl((a), (b), (c))
+#else
+#define ATTN5_MFMA(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_f16((a), (b), (c), 0, 0, 0)
+#endif
+
 namespace dllm {
 namespace {
 
@@ -461,7 +482,7 @@ kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__
 #pragma unroll
             for (int t = 0; t < kD / 16; ++t) {
                 const half8_t kf = *reinterpret_cast<const half8_t *>(&kb_[32 * u + ql][16 * t + 8 * hh]);
-                st[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[t], st[u], 0, 0, 0);
+                st[u] = ATTN5_MFMA(kf, qf[t], st[u]);
             }
         }
     };
@@ -555,7 +576,7 @@ kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__
                     asm volatile("" ::"v"(kf));
                     sn[u][t] += 1.0f;
                 } else {
-                    sn[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[t], sn[u], 0, 0, 0);
+                    sn[u] = ATTN5_MFMA(kf, qf[t], sn[u]);
                 }
             }
         }
@@ -634,7 +655,7 @@ kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__
                 if constexpr (LAB & 4) {   // measurement only: no PV MFMAs (operands kept live)
                     asm volatile("" ::"v"(vb), "v"(pa));
                 } else {
-                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(pa, vb, o[dt], 0, 0, 0);
+                    o[dt] = ATTN5_MFMA(pa, vb, o[dt]);
                 }
             }
         }
