@@ -1279,6 +1279,13 @@ int launch_horner_rows_gemm(const HornerGemmArgs &a, int rows, int y_f32, hipStr
 
 int launch_horner_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
 #if DLLM_LAB
+    if (a.lab == 26 || a.lab == 27) {   // lab A/B: the 16x16x32 kernel without the stagger (26) /
+                                        // with one DMA burst per stage instead of spread pieces (27)
+        if (a.lab == 26) launch_horner16_t<256 | 1024>(a, y_f32, st);
+        else launch_horner16_t<1 | 1024>(a, y_f32, st);
+        DLLM_LAUNCH_CHECK();
+        return DLLM_OK;
+    }
     if (a.lab == 25) {   // lab A/B: the 16x16x32 kernel with MODE bit 11 (2 % slower on one box:
                          // profiles/r04_horner/h16_early_dequant_ab.json)
         launch_horner16_t<1 | 256 | 1024 | 2048>(a, y_f32, st);
