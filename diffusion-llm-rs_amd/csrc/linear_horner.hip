@@ -835,7 +835,7 @@ __global__ void __launch_bounds__(512, 1)
 wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdev,
                    const uint32_t *__restrict__ sz, const float *__restrict__ hr, const float *__restrict__ sf,
                    const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad, int nbm, int nbn,
-                   PSampleEpi epi) {
+                   PSampleEpi epi, int grows = 0) {
     constexpr bool STAG = MODE & 1;
     using L = H16<TB>;
     constexpr int kStage = L::kStage, kXB = L::kXB, kKPS = L::kKPS;
@@ -845,7 +845,13 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
     const int nb = nbm * nbn, orig = blockIdx.x;
     const int xcd = orig % kXCDs, q8 = nb / kXCDs, r8 = nb % kXCDs;
     const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / kXCDs;
-    const int bm = tile / nbn, bn = tile % nbn;
+    int bm = tile / nbn, bn = tile % nbn;
+    if (DLLM_LAB && (grows == 2 || grows == 4 || grows == 8 || grows == 16) && nb == 256 && nbm == 16 && nbn == 16) {
+        // lab A/B: each XCD's 32 tiles as grows row-blocks x (32 / grows) column-blocks
+        const int gc = 32 / grows, reg = tile / 32, loc = tile % 32, per_row = 16 / gc;
+        bm = (reg / per_row) * grows + loc / gc;
+        bn = (reg % per_row) * gc + loc % gc;
+    }
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int m0 = bm * 16 * TB, n0 = bn * 256;
@@ -1218,19 +1224,19 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
 }
 
 template <int MODE, int TB = 16>
-void launch_horner16_t(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
+void launch_horner16_t(const HornerGemmArgs &a, int y_f32, hipStream_t st, int grows = 0) {
     const int nbm = (a.M + 16 * TB - 1) / (16 * TB), nbn = a.Npad / 256;
     const unsigned nb = static_cast<unsigned>(nbm * nbn);
     const PSampleEpi ep = a.epi ? *a.epi : PSampleEpi{};
     if (a.epi)
         wq_horner16_kernel<float, 1, MODE, TB><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
-                                                               a.epi->x_prev, a.N, a.Npad, nbm, nbn, ep);
+                                                               a.epi->x_prev, a.N, a.Npad, nbm, nbn, ep, grows);
     else if (y_f32)
         wq_horner16_kernel<float, 0, MODE, TB><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
-                                                               static_cast<float *>(a.Y), a.N, a.Npad, nbm, nbn, ep);
+                                                               static_cast<float *>(a.Y), a.N, a.Npad, nbm, nbn, ep, grows);
     else
         wq_horner16_kernel<__half, 0, MODE, TB><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
-                                                                static_cast<__half *>(a.Y), a.N, a.Npad, nbm, nbn, ep);
+                                                                static_cast<__half *>(a.Y), a.N, a.Npad, nbm, nbn, ep, grows);
 }
 
 template <int MODE>
@@ -1279,6 +1285,11 @@ int launch_horner_rows_gemm(const HornerGemmArgs &a, int rows, int y_f32, hipStr
 
 int launch_horner_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
 #if DLLM_LAB
+    if (a.lab == 28) {   // lab A/B: the 16x16x32 kernel with 4 x 8 XCD tile groups
+        launch_horner16_t<1 | 256 | 1024>(a, y_f32, st, 4);
+        DLLM_LAUNCH_CHECK();
+        return DLLM_OK;
+    }
     if (a.lab == 26 || a.lab == 27) {   // lab A/B: the 16x16x32 kernel without the stagger (26) /
                                         // with one DMA burst per stage instead of spread pieces (27)
         if (a.lab == 26) launch_horner16_t<256 | 1024>(a, y_f32, st);

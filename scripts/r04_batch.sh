@@ -42,7 +42,7 @@ for s in ${STEPS:-tests chain quant horner shard}; do
           AB_M=3000 step h128_3000 120 python scripts/horner_ab.py -1 323
           AB_M=4096 AB_N=2048 step h128_shard2 120 python scripts/horner_ab.py -1 323
 ;;
-    h16) step h16 200 python scripts/horner_ab.py -1 326 327 -1 326 327;;
+    h16) step h16 200 python scripts/horner_ab.py -1 328 -1 328 -1 328;;
     blas) step blas 120 python scripts/blas_shapes.py
           LIBS=diffusion-llm-rs_amd/lib/libdllm_hip.so ROUNDS=2 step shard_ab 200 python scripts/gemm_ab.py;;
     tp) DLLM_BENCH_BACKEND=gloo step tp_trace 400 rocprofv3 --kernel-trace -d $O/tp -o kt --output-format csv -- python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --tp-steps 4 --no-cpu;;
