@@ -1276,12 +1276,14 @@ int launch_horner_kg2_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
     return DLLM_OK;
 }
 
+#if DLLM_LAB
 int launch_horner_rows_gemm(const HornerGemmArgs &a, int rows, int y_f32, hipStream_t st) {
     if (rows != 128) return fail(DLLM_ERR_INVALID_PARAMS, "Horner tiles: 128 rows");
     launch_horner16_t<1 | 256, 8>(a, y_f32, st);
     DLLM_LAUNCH_CHECK();
     return DLLM_OK;
 }
+#endif
 
 int launch_horner_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
 #if DLLM_LAB

@@ -1954,17 +1954,14 @@ bool horner_ready(const dllm_linear *hc, int M, hipStream_t st) {
 // against the fold form on those grids it measured -2.8 % on one box and +8 % on another (M = 2048:
 // 64.9 vs 66.7 us, 72.5 vs 67.0 us; profiles/r04_horner/), so the fold form stays the product path.
 // Returns the tile rows, 0 = not applicable.
-int horner_rows(const dllm_linear *hc, int M) {
 #if DLLM_LAB
+int horner_rows(const dllm_linear *hc, int M) {
     const int np = static_cast<int>(hc->Npad);
     if (hc->variant != 323 || !horner_shape(hc) || hc->hstate != 1) return 0;
     if (((M + 127) / 128) * (np / 256) >= kCUs) return 128;
-#else
-    (void)hc;
-    (void)M;
-#endif
     return 0;
 }
+#endif
 
 // The KG2 Horner kernel (256 x 128 tiles, two k-groups): where neither the 256 x 256 Horner grid
 // nor the fold form's 128 x 256 grid fills a round but the 256 x 128 grid does (N = 4096: M
@@ -2049,11 +2046,13 @@ int launch_prefill_auto(const dllm_linear *h, const __half *X, int M, YT *Y, hip
                                    (int)h->Npad, epi};
             return launch_horner_kg2_gemm(a, std::is_same<YT, float>::value ? 1 : 0, st);
         }
-        if (const int rows = BITS == 4 ? horner_rows(h, M) : 0) {
+#if DLLM_LAB
+        if (const int rows = BITS == 4 ? horner_rows(h, M) : 0) {   // lab A/B 323 only
             const HornerGemmArgs a{X, M, (int)h->K, h->wdev, h->sz, h->hr, h->sf, h->bias, Y, (int)h->N,
                                    (int)h->Npad, epi};
             return launch_horner_rows_gemm(a, rows, std::is_same<YT, float>::value ? 1 : 0, st);
         }
+#endif
         ExactGemmArgs a = exact_args(h, X, M, Y, epi);
 #if DLLM_EXACT_HORNER   // A/B build: the 128 x 256 exact tiles in Horner form too
         if (BITS == 4 && ensure_horner(h, st)) a.hr = h->hr;
