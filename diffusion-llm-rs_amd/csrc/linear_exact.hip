@@ -957,7 +957,15 @@ int launch_exact_bits(const ExactGemmArgs &a, hipStream_t st) {
 #if DLLM_EXACT_KG2
     // tile-starved grids: 128 x 128 (or 64 x 128) tiles with two k-groups of 4 waves per block
     if constexpr (G64 == 2 && BITS == 4 && DLLM_EXACT_WREG) {
-        // (lab A/B policy 5: 64 x 128 tiles, two blocks per CU, where 128 x 128 tiles give one round)
+        // (lab A/B policy 5: 64 x 128 tiles, two blocks per CU, where 128 x 128 tiles give one round;
+        // 6 / 7: the 128 x 128 tiles with 64-deep stages in a 4- / 3-stage ring instead of 128-deep
+        // stages in a 2-stage ring)
+#if DLLM_LAB
+        if (tiles >= kCUs && tiles < 2 * kCUs && ngroups % 2 == 0 && a.lab_policy == 6)
+            return launch_exact_tile<BITS, YT, 4, 4, 1, 2, EPI, false, 1, 4, 2>(a, 1, st);
+        if (tiles >= kCUs && tiles < 2 * kCUs && ngroups % 2 == 0 && a.lab_policy == 7)
+            return launch_exact_tile<BITS, YT, 4, 4, 1, 2, EPI, false, 1, 3, 2>(a, 1, st);
+#endif
         if (tiles >= kCUs && tiles < 2 * kCUs && ngroups % 2 == 0 && a.lab_policy != 5)
             return launch_exact_tile<BITS, YT, 4, 4, 2, 1, EPI, false, 1, 2, 2>(a, 1, st);
         const int t64 = ((a.M + 63) / 64) * (a.Npad / 128);

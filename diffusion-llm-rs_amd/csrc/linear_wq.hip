@@ -2019,7 +2019,7 @@ inline ExactGemmArgs exact_args(const dllm_linear *h, const __half *X, int M, vo
                     (int)h->group, epi};
 #if DLLM_LAB
     a.tm = h->variant == 15 ? 1 : 0;
-    a.lab_policy = h->variant == 28 ? 1 : (h->variant >= 300 && h->variant <= 302 ? h->variant - 298 : (h->variant == 329 ? 5 : 0));
+    a.lab_policy = h->variant == 28 ? 1 : (h->variant >= 300 && h->variant <= 302 ? h->variant - 298 : (h->variant == 329 ? 5 : (h->variant == 330 ? 6 : (h->variant == 331 ? 7 : 0))));
 #endif
     return a;
 }
@@ -2466,8 +2466,8 @@ int dllm_linear_set_kernel_variant(dllm_linear_t h, int variant) {
         h->pplab = (variant - 100) % 32;
         return DLLM_OK;
     }
-    if (variant < -1 || (variant > 15 && (variant < 24 || variant > 31) && (variant < 300 || variant > 329 || variant == 313)))
-        return fail(DLLM_ERR_INVALID_PARAMS, "variant must be -1..15, 24..31, 300..312 or 314..329 (16..23, 32..95, 100..195, 200..263: ablations)");
+    if (variant < -1 || (variant > 15 && (variant < 24 || variant > 31) && (variant < 300 || variant > 331 || variant == 313)))
+        return fail(DLLM_ERR_INVALID_PARAMS, "variant must be -1..15, 24..31, 300..312 or 314..331 (16..23, 32..95, 100..195, 200..263: ablations)");
     h->variant = variant;
     h->dlab = h->rlab = h->pplab = h->dcfg = 0;
     return DLLM_OK;
