@@ -8,7 +8,9 @@ to each group's partial sum).  The rounded-weight mode (DLLM_PRECISION_F16W) is 
 as ``f16_weights``.  Synthetic data: X ~ N(0,1), W ~ 0.02 N(0,1), b = 0 (SimpleDiffusionModel::new,
 diffuse-llm-rs/src/lib.rs:791-801).
 
-Multi-GPU (--gpus N, launched by torch.distributed.run, one process per GPU): the SAME fixed
+Multi-GPU (--gpus N, one process per GPU: launched by torch.distributed.run, or -- when WORLD_SIZE
+is unset -- by bench.py itself, which starts N fresh rank processes before anything touches the
+GPU; a WORLD_SIZE that differs from --gpus is an error): the SAME fixed
 4096-token step is split over the ranks by hidden (output) dimension -- column-parallel, rank r
 owns the group-aligned columns [n0, n1) of W (parallel.ColumnParallelLinear), X replicated --
 so ``value`` = 4096 tokens per step / max-over-ranks step time ("scaling": "strong").  No
@@ -380,12 +382,65 @@ def m_sweep(lin, K, N, bits, group, torch, dev, stream, n_layers=40):
     return {"layers": n_layers, "timing": "HIP graph replay, HIP events", "rows": rows}
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, argv, script=None):
+    """``bench.py --gpus N`` run without a launcher: start N fresh rank processes of this script
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their env, rendezvous on 127.0.0.1) and return the
+    first non-zero exit code (else 0).  Called before anything imports torch or touches the GPU, and
+    the children are new processes, never an exec of this one; rank 0 prints the JSON line."""
+    import signal
+    import subprocess
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, str(script or Path(__file__).resolve()), *argv], env=env))
+    rc = 0
+    try:
+        for p in procs:
+            c = p.wait()
+            if c != 0 and rc == 0:
+                rc = c
+                for q in procs:          # one rank failed: the others would hang in a collective
+                    if q.poll() is None:
+                        q.send_signal(signal.SIGTERM)
+    except KeyboardInterrupt:
+        for q in procs:
+            if q.poll() is None:
+                q.send_signal(signal.SIGTERM)
+        raise
+    return rc if rc >= 0 else 128 - rc
+
+
+def check_world(gpus, env):
+    """The job's world size must be the --gpus it was asked for: returns (world, error or None).
+    WORLD_SIZE unset means a single process, i.e. --gpus 1 (--gpus > 1 is spawned by main)."""
+    world = int(env.get("WORLD_SIZE", "1"))
+    if world != gpus:
+        return world, (f"bench.py: --gpus {gpus} but WORLD_SIZE={world}: the launcher started a different number "
+                       f"of ranks than asked for")
+    return world, None
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    world, err = check_world(args.gpus, os.environ)
+    if err:
+        sys.exit(err)
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # DLLM_BENCH_BACKEND=gloo + device = local % device_count: a rehearsal of the N > 1 path with

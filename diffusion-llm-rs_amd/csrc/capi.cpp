@@ -7,6 +7,7 @@
 #include <mutex>
 #include <string>
 #include <tuple>
+#include <vector>
 
 #include "dllm_quant.h"
 
@@ -21,62 +22,76 @@ int fail(int code, const std::string &msg) {
     return code;
 }
 
-float *device_workspace(hipStream_t st, size_t bytes, int slot) {
-    static std::mutex mu;
-    static std::map<std::tuple<int, hipStream_t, int>, std::pair<float *, size_t>> pool;
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    std::lock_guard<std::mutex> lk(mu);
-    auto &e = pool[{dev, st, slot}];
-    if (e.second >= bytes) return e.first;
+// Grow-only per-(device, stream, slot) workspaces.  A buffer handed out while its stream was being
+// captured is referenced by that graph for as long as the graph lives, so once captured it is never
+// freed: a later, larger request on the same slot allocates a new buffer and RETIRES the captured one
+// (kept until process exit), so replaying an earlier graph after an eager call of a larger shape
+// still reads and writes valid memory (its own old buffer, which no eager call uses any more).
+// Buffers never seen by a capture are freed on growth as before.
+namespace {
+struct Workspace {
+    void *p = nullptr;
+    size_t bytes = 0;
+    bool captured = false;
+};
+std::vector<void *> &retired_workspaces() {
+    static std::vector<void *> v;   // captured buffers replaced by larger ones: alive for graph replays
+    return v;
+}
+bool stream_capturing(hipStream_t st) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     (void)hipStreamIsCapturing(st, &cs);
-    if (cs != hipStreamCaptureStatusNone) {
-        fail(DLLM_ERR_HIP, "device workspace must be sized before stream capture (run the shape once first)");
+    return cs != hipStreamCaptureStatusNone;
+}
+// Returns the slot's buffer of at least `bytes` (zeroed when `zero`), or nullptr with the error set.
+void *grow_workspace(Workspace &e, hipStream_t st, size_t bytes, bool zero, const char *what) {
+    const bool capturing = stream_capturing(st);
+    if (e.bytes >= bytes) {
+        if (capturing) e.captured = true;
+        return e.p;
+    }
+    if (capturing) {
+        fail(DLLM_ERR_HIP, std::string(what) + " must be sized before stream capture (run the shape once first)");
         return nullptr;
     }
-    if (e.first) {
+    if (e.p) {
         if (hipStreamSynchronize(st) != hipSuccess) return nullptr;
-        (void)hipFree(e.first);
-        e = {nullptr, 0};
+        if (e.captured) retired_workspaces().push_back(e.p);
+        else (void)hipFree(e.p);
+        e = Workspace{};
     }
-    float *p = nullptr;
-    if (hipMalloc(reinterpret_cast<void **>(&p), bytes) != hipSuccess) {
-        fail(DLLM_ERR_HIP, "hipMalloc of a device workspace failed");
+    void *p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+        fail(DLLM_ERR_HIP, std::string("hipMalloc of the ") + what + " failed");
         return nullptr;
     }
-    e = {p, bytes};
+    if (zero && hipMemsetAsync(p, 0, bytes, st) != hipSuccess) {
+        (void)hipFree(p);
+        fail(DLLM_ERR_HIP, std::string("zeroing the ") + what + " failed");
+        return nullptr;
+    }
+    e.p = p;
+    e.bytes = bytes;
     return p;
+}
+std::mutex g_ws_mu;   // guards both pools and the retired list
+}  // namespace
+
+float *device_workspace(hipStream_t st, size_t bytes, int slot) {
+    static std::map<std::tuple<int, hipStream_t, int>, Workspace> pool;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    return static_cast<float *>(grow_workspace(pool[{dev, st, slot}], st, bytes, false, "device workspace"));
 }
 
 unsigned *zeroed_counters(hipStream_t st, size_t n) {
-    static std::mutex mu;
-    static std::map<std::pair<int, hipStream_t>, std::pair<unsigned *, size_t>> pool;
+    static std::map<std::pair<int, hipStream_t>, Workspace> pool;
     int dev = 0;
     (void)hipGetDevice(&dev);
-    std::lock_guard<std::mutex> lk(mu);
-    auto &e = pool[{dev, st}];
-    if (e.second >= n) return e.first;
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    (void)hipStreamIsCapturing(st, &cs);
-    if (cs != hipStreamCaptureStatusNone) {
-        fail(DLLM_ERR_HIP, "hand-off words must be allocated before stream capture (run the shape once first)");
-        return nullptr;
-    }
-    if (e.first) {
-        if (hipStreamSynchronize(st) != hipSuccess) return nullptr;
-        (void)hipFree(e.first);
-        e = {nullptr, 0};
-    }
-    unsigned *p = nullptr;
+    std::lock_guard<std::mutex> lk(g_ws_mu);
     const size_t cap = std::max<size_t>(n, 64);
-    if (hipMalloc(reinterpret_cast<void **>(&p), cap * sizeof(unsigned)) != hipSuccess ||
-        hipMemsetAsync(p, 0, cap * sizeof(unsigned), st) != hipSuccess) {
-        fail(DLLM_ERR_HIP, "hipMalloc of the hand-off words failed");
-        return nullptr;
-    }
-    e = {p, cap};
-    return p;
+    return static_cast<unsigned *>(grow_workspace(pool[{dev, st}], st, cap * sizeof(unsigned), true, "hand-off words"));
 }
 
 }  // namespace dllm

@@ -378,6 +378,9 @@ int launch_quantize_resident(const float *const *x, const size_t *n, int nt, con
     A.partials = static_cast<float2 *>(ws);
     A.sync = zeroed_counters(st, 4);
     if (!A.sync) return DLLM_ERR_HIP;
+    // sync[2] is the hand-off timeout word: a timed-out launch writes NaN params (so its failure is
+    // visible in its own output); clearing it per launch keeps one timeout from poisoning the next
+    if (hipMemsetAsync(A.sync + 2, 0, sizeof(unsigned), st) != hipSuccess) return fail(DLLM_ERR_HIP, "hipMemsetAsync");
     A.nb = nb;
 #if DLLM_LAB
     if (const char *e = std::getenv("DLLM_RES_LAB")) A.lab = std::atoi(e);

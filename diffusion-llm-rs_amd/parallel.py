@@ -27,7 +27,10 @@ with the partition logic (their helpers, which put all G shards behind the unsha
 live in tests/tp_emulation.py).  The local layer is pluggable (``local_factory``): on the GPU it is
 ``QuantLinear`` (HIP kernels: the GEMM and the row-parallel epilogue ``bias_cast``); the CPU
 multi-process tests pass the oracle's restatement so the partition and collective logic is checked
-under gloo without a GPU.
+under gloo without a GPU.  A local layer is built as ``local_factory(W_shard, bias_shard, bits,
+group)`` and called as ``local(x, out_dtype=..., out=...)``; it may provide
+``bias_cast(y, bias, out_dtype)`` for the row-parallel epilogue (QuantLinear's is the library
+kernel), otherwise that epilogue is ``(y + bias).to(out_dtype)``.
 """
 from __future__ import annotations
 
@@ -120,7 +123,6 @@ class RowParallelLinear:
         self.k0, self.k1 = row_range(K, self.world, self.rank, group)
         self.bias = bias
         self.local = local_factory(W[self.k0:self.k1].contiguous(), None, bits, group)
-        self._pads = {}   # zero-padded f32 partial buffers of the rs_ag form, per (chunk, rows, device)
 
     def partial(self, x: torch.Tensor, x_is_shard: bool = False, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """This rank's un-reduced f32 partial X[:, k0:k1] . W^[k0:k1, :] (no bias), into ``out`` when given."""
@@ -133,13 +135,22 @@ class RowParallelLinear:
         """The bias, once, after the reduction, and the output cast: the local layer's epilogue
         (``QuantLinear.bias_cast`` = dllm_bias_cast, lib.rs:812)."""
         bias = None if self.bias is None else self.bias.to(y.device, torch.float32)
-        return self.local.bias_cast(y, bias, out_dtype)
+        cast = getattr(self.local, "bias_cast", None)
+        if cast is None or out_dtype not in (torch.float16, torch.float32):
+            # a local layer without the library epilogue (a custom local_factory), or an output type
+            # the kernel does not store: the same sum in f32, then the cast
+            yb = y if bias is None else y + bias
+            return yb.to(out_dtype)
+        return cast(y, bias, out_dtype)
 
-    def _padded(self, c: int, Mp: int, N: int, device) -> torch.Tensor:
-        key = (c, Mp, N, str(device))
-        if key not in self._pads:   # rows past the chunk's stay zero: the GEMM writes only the first M
-            self._pads[key] = torch.zeros(Mp, N, dtype=torch.float32, device=device)
-        return self._pads[key]
+    @staticmethod
+    def _padded(M: int, Mp: int, N: int, device) -> torch.Tensor:
+        """A fresh [Mp, N] f32 buffer whose rows M.. (the padding) are zero; the GEMM writes rows
+        ..M.  Allocated per call from the stream-ordered caching allocator, so nothing is shared
+        between concurrent forwards and nothing accumulates per sequence length."""
+        y = torch.empty(Mp, N, dtype=torch.float32, device=device)
+        y[M:].zero_()
+        return y
 
     def forward(self, x: torch.Tensor, out_dtype=torch.float16, x_is_shard: bool = False,
                 chunks: int = 1) -> torch.Tensor:
@@ -184,7 +195,7 @@ class RowParallelLinear:
             if Mp == M:
                 y = self.partial(xc, True)
             else:   # the chunk's rows padded to a multiple of the world with zero rows
-                y = self._padded(c, Mp, self.N, xc.device)
+                y = self._padded(M, Mp, self.N, xc.device)
                 self.partial(xc, True, out=y[:M])
             mine = torch.empty(Mp // self.world, y.shape[1], dtype=torch.float32, device=y.device)
             work = dist.reduce_scatter_tensor(mine, y, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)

@@ -152,12 +152,23 @@ def quantize_kv_with_extremes(keys: torch.Tensor, values: torch.Tensor, red: tor
 
 def bias_cast(y: torch.Tensor, bias: torch.Tensor | None, out_dtype=torch.float16, out: torch.Tensor | None = None):
     """dllm_bias_cast: ``y + bias`` (f32) stored as ``out_dtype`` -- a row-parallel layer's epilogue
-    after its partial sums are reduced (diffuse-llm-rs/src/lib.rs:812)."""
+    after its partial sums are reduced (diffuse-llm-rs/src/lib.rs:812).  ``y`` must be a contiguous
+    2-D f32 device tensor and the output f16 or f32 (the kernel's two store types); anything else
+    raises ``UnsupportedOperation`` / ``ShapeMismatch`` rather than storing the wrong element size."""
+    if y.dim() != 2 or y.dtype != torch.float32 or not y.is_cuda or not y.is_contiguous():
+        raise _lib.UnsupportedOperation("bias_cast: y must be a contiguous 2-D float32 device tensor")
     M, N = y.shape
+    dtype = out.dtype if out is not None else out_dtype
+    if dtype not in (torch.float16, torch.float32):
+        raise _lib.UnsupportedOperation(f"bias_cast: output dtype {dtype} (only float16 / float32)")
     if out is None:
-        out = torch.empty(M, N, dtype=out_dtype, device=y.device)
-    dt = _lib.F16 if out.dtype == torch.float16 else _lib.F32
+        out = torch.empty(M, N, dtype=dtype, device=y.device)
+    elif tuple(out.shape) != (M, N) or not out.is_contiguous() or out.device != y.device:
+        raise _lib.ShapeMismatch(f"bias_cast: out must be a contiguous [{M}, {N}] tensor on {y.device}")
+    dt = _lib.F16 if dtype == torch.float16 else _lib.F32
     b = None if bias is None else _dev(bias, torch.float32)
+    if b is not None and b.numel() != N:
+        raise _lib.ShapeMismatch(f"bias_cast: bias has {b.numel()} elements, y has {N} columns")
     check(_lib.load().dllm_bias_cast(_ptr(y), M, N, None if b is None else _ptr(b), _ptr(out), dt, _stream()))
     return out
 

@@ -251,7 +251,9 @@ int dllm_linear_create_quantized_ex(const uint8_t *packed_codes, const float *sc
  * (M roughly 65..1000 at N = 4096) split K into slices whose f32 partials are combined in slice
  * order (deterministic) through a per-(device, stream) workspace.  Both workspaces only grow and
  * are allocated on the first call that needs them, which therefore must precede stream capture.
- * Otherwise the call only launches kernels on `stream`: it never synchronises, and the kernel a
+ * A workspace a capture has used is never freed: when a later, larger call on the same stream grows
+ * it, the captured buffer is retired (kept for the process lifetime), so an earlier graph still
+ * replays on valid memory.  Otherwise the call only launches kernels on `stream`: it never synchronises, and the kernel a
  * shape runs (hence its result bits) does not depend on call history or on capture.
  * DLLM_PRECISION_EXACT, int4 g128, on grids of >= 256 tiles of 256 x 256 (M >= 4096 at N = 4096)
  * runs the Horner-form kernel when the handle's create accepted its ratios, else the fold form

@@ -1010,6 +1010,56 @@ def test_bias_cast(dllm, torch):
         assert torch.equal(yy, ref)
 
 
+def test_bias_cast_refuses_other_dtypes(dllm, torch):
+    """The kernel stores f16 or f32 only: a bf16 / f64 output, a non-f32 or non-contiguous y and a
+    wrong-size bias are refused before any launch (a bf16 output used to get f32 stores
+    past the end of its 2-byte buffer)."""
+    y = torch.randn(64, 128, device="cuda")
+    b = torch.randn(128, device="cuda")
+    for dt in (torch.bfloat16, torch.float64):
+        with pytest.raises(dllm.UnsupportedOperation):
+            dllm.quantization.bias_cast(y, b, dt)
+        with pytest.raises(dllm.UnsupportedOperation):
+            dllm.quantization.bias_cast(y, b, out=torch.empty(64, 128, dtype=dt, device="cuda"))
+    with pytest.raises(dllm.UnsupportedOperation):
+        dllm.quantization.bias_cast(y.half(), b, torch.float16)
+    with pytest.raises(dllm.UnsupportedOperation):
+        dllm.quantization.bias_cast(y.t(), b, torch.float16)
+    with pytest.raises(dllm.ShapeMismatch):
+        dllm.quantization.bias_cast(y, b[:100], torch.float16)
+    with pytest.raises(dllm.ShapeMismatch):
+        dllm.quantization.bias_cast(y, b, out=torch.empty(64, 127, device="cuda"))
+
+
+def test_graph_replay_after_workspace_growth(dllm, torch, orc):
+    """A graph captured with an f32-X forward (the f32 -> f16 staging workspace of the stream) stays
+    valid after a LARGER eager f32 forward on the same stream grew that workspace: the captured
+    buffer is retired, not freed, so the replay reproduces its first result bit for bit."""
+    K, N = 512, 256
+    g = torch.Generator(device="cuda").manual_seed(77)
+    lin = dllm.QuantLinear.from_weight(0.02 * torch.randn(K, N, device="cuda", generator=g), None, 4, 128)
+    s = torch.cuda.Stream()
+    Xs = torch.randn(96, K, device="cuda", generator=g)            # f32 X: staged to f16 in the workspace
+    Xl = torch.randn(4096, K, device="cuda", generator=g)
+    Ys = torch.empty(96, N, device="cuda")
+    with torch.cuda.stream(s):
+        lin(Xs, out=Ys)                                             # sizes the workspace for the small shape
+        torch.cuda.current_stream().synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=s):
+            lin(Xs, out=Ys)
+        graph.replay()
+        s.synchronize()
+        first = Ys.clone()
+        Ys.zero_()
+        big = lin(Xl, out_dtype=torch.float32)                      # grows the same stream's workspace
+        graph.replay()
+        s.synchronize()
+    assert torch.equal(Ys, first)
+    assert bool(torch.isfinite(big).all())
+    lin.close()
+
+
 def _two_pass_ref(q, x, bits):
     """Codes and params by an independent device path: the min/max kernels (tensor_extremes), the
     params of :49-56, then the map alone (quantize_tensor_with_params)."""
