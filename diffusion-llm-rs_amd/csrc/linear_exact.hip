@@ -19,6 +19,7 @@
 // pair and f32 scale words) through a 3-stage ring with counted vmcnt waits and raw s_barrier,
 // as wq_gemm8_kernel.  Weight layout: the prefill ("fragment-major") layout of linear_wq.hip.
 #include "linear_common.hpp"
+#include "stamp.hpp"
 
 #ifndef DLLM_LAB
 #define DLLM_LAB 0
@@ -61,6 +62,18 @@
 #define DLLM_EXACT_HORNER 0
 #endif
 
+// DLLM_EXACT_KG_COAL = 1: on the k-group tiles (KG >= 2) the f16 epilogue is the coalesced LDS-staged
+//   one, stored by all KG x NW waves (round 5, profiles/r05_shard/: 4096 x 1024 40.2 -> 38.1 us,
+//   2048 x 2048 40.6 -> 38.6 us, rocprof means on one box); 0 = k-group 0's row-per-lane stores.
+#ifndef DLLM_EXACT_KG_COAL
+#define DLLM_EXACT_KG_COAL 1
+#endif
+// DLLM_EXACT_SPREAD = 1 (A/B): the stage's LDS-DMA / weight loads are issued a few per substep (in
+// front of that substep's MFMAs) instead of as one burst at the head of the step.
+#ifndef DLLM_EXACT_SPREAD
+#define DLLM_EXACT_SPREAD 0
+#endif
+
 #include <algorithm>
 #include <type_traits>
 #include <utility>
@@ -91,6 +104,10 @@ constexpr int kExactMF = 1;
 
 namespace dllm {
 namespace {
+
+#if DLLM_STAMP
+DLLM_STAMP_BUFFER(g_stamp_exact);   // phase stamps of wq_gemm_exact_kernel (stamp build only)
+#endif
 
 // A stage holds SPS consecutive 64-deep slabs (X tile, weight words) plus the group's zero-point
 // pairs and f32 scales; SPS = 2 makes a stage one 128-row group (one fold and one barrier per group).
@@ -169,6 +186,42 @@ __device__ __forceinline__ void store_tile16x_f16_lds(uint8_t *img, int cap, con
     }
 }
 
+// Two-k-group f16 epilogue: k-group 0 (which holds the combined sums) writes the f16 tile (acc +
+// bias) into `img` as 16-B row chunks XORed with the row, then every wave of the block stores whole
+// rows with 16-B lanes -- the coalesced store of store_tile_f16_lds with KG x the storing waves.
+template <int NW, int MR, int KG>
+__device__ __forceinline__ void store_tile_f16_lds_kg(uint8_t *img, const float16_t (&acc)[MR], const float4 (&bv)[4],
+                                                      __half *Y, int N, int m0, int n0, int wave, int kg, int lane) {
+    constexpr int kRowB = 64 * NW, kCpr = 4 * NW, kRows = 32 * MR;
+    if (kg == 0) {
+        const int hsel = lane >> 5, c0 = wave * 4;
+#pragma unroll
+        for (int r = 0; r < MR; ++r) {
+            const int t = r * 32 + (lane & 31);
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd) {
+                const int pc = (c0 + qd) ^ (t & (kCpr - 1));
+                union { __half h[4]; uint2 u; } pk;
+                pk.h[0] = __float2half_rn(acc[r][4 * qd + 0] + bv[qd].x);
+                pk.h[1] = __float2half_rn(acc[r][4 * qd + 1] + bv[qd].y);
+                pk.h[2] = __float2half_rn(acc[r][4 * qd + 2] + bv[qd].z);
+                pk.h[3] = __float2half_rn(acc[r][4 * qd + 3] + bv[qd].w);
+                *reinterpret_cast<uint2 *>(img + t * kRowB + pc * 16 + hsel * 8) = pk.u;
+            }
+        }
+    }
+    __syncthreads();
+    constexpr int kRowsPerInst = 1024 / kRowB;
+    const int c = lane % kCpr;
+    for (int t0 = (kg * NW + wave) * kRowsPerInst; t0 < kRows; t0 += NW * KG * kRowsPerInst) {
+        const int t = t0 + lane / kCpr;
+        const uint4 v = *reinterpret_cast<const uint4 *>(img + t * kRowB + ((c ^ (t & (kCpr - 1))) * 16));
+        typedef unsigned int u4nt __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(u4nt{v.x, v.y, v.z, v.w},
+                                    reinterpret_cast<u4nt *>(Y + static_cast<size_t>(m0 + t) * N + n0 + 8 * c));
+    }
+}
+
 // S16: the MFMAs are 16x16x32 (not TM / HORN).  The chip holds a higher clock on that shape at the
 // same FLOPs (MI355X_MICROARCH.md, DVFS give-back item 7); per wave the 32 columns x 32 MR tokens are
 // 2 column blocks x 2 MR token blocks of 16 x 16 (acc16 / tacc16: the same registers as acc / tacc).
@@ -212,6 +265,17 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
     const int bm = first + in_grp % gm, bn = in_grp / gm;
 
     const int tid = threadIdx.x, lane = tid & 63;
+    DLLM_STAMP_RT(g_stamp_exact, stamp::kRtEntry);
+    DLLM_STAMP_AT(g_stamp_exact, 0);
+    DLLM_STAMP_IDS(g_stamp_exact);
+#if DLLM_STAMP
+    struct StampEnd {
+        __device__ ~StampEnd() {
+            DLLM_STAMP_AT(g_stamp_exact, stamp::kEnd);
+            DLLM_STAMP_RT(g_stamp_exact, stamp::kRtEnd);
+        }
+    } stamp_end;
+#endif
     const int kg = KG == 1 ? 0 : __builtin_amdgcn_readfirstlane((tid >> 6) / NW);
     const int wave = __builtin_amdgcn_readfirstlane((tid >> 6) - kg * NW);   // wave within the k-group
     const int m0 = bm * kBMt, n0 = bn * kBNt;
@@ -278,6 +342,26 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
         const uint32_t goff = u((slab0 / spg + pg) * static_cast<uint32_t>(Npad) * 4);
         if (has_sz) blds16_asm(prs, poff, goff, u(base + SL::kX + SL::kW + pg * 1024));
         if (has_sf) blds16_asm(prs, poff, goff, u(base + SL::kX + SL::kW + SL::kSZ + pg * 1024));
+    };
+    // The same loads one piece at a time (SPREAD): pieces 0 .. SPS kR1 - 1 are X, then the SPS weight
+    // loads, then the group's {zp, scale} words; issue order (hence every vmcnt count) is stage()'s.
+    constexpr int kPieces = SPS * SL::kR1 + SPS + 1;
+    auto stage_piece = [&](uint8_t *sb, unsigned kt, auto slot_tag, auto p_tag) __attribute__((always_inline)) {
+        constexpr int slot = decltype(slot_tag)::value, p = decltype(p_tag)::value;
+        const uint32_t base = u(lds_addr(sb));
+        const unsigned slab0 = (kt + kt0) * SPS;
+        if constexpr (p < SPS * SL::kR1) {
+            constexpr int s = p / SL::kR1, i = p % SL::kR1;
+            blds16_asm(xrs, xoff[i], u((slab0 + s) * kBK * 2), u(base + s * SL::kX1 + wv * 1024 + i * NW * 1024));
+        } else if constexpr (p < SPS * SL::kR1 + SPS) {
+            constexpr int s = p - SPS * SL::kR1;
+            static_assert(WREG, "spread issue: register-staged weight words only");
+            bload16_asm(wq[slot][s], wrs, woff, u((slab0 + s) * 64 * BITS * 4));
+        } else {
+            const uint32_t goff = u((slab0 / spg + pg) * static_cast<uint32_t>(Npad) * 4);
+            if (has_sz) blds16_asm(prs, poff, goff, u(base + SL::kX + SL::kW + pg * 1024));
+            if (has_sf) blds16_asm(prs, poff, goff, u(base + SL::kX + SL::kW + SL::kSZ + pg * 1024));
+        }
     };
     // Counted wait leaving the newest stage's DMAs (this wave's own count) in flight.
     // (RING > 3: the RING - 2 newest stages stay in flight.)
@@ -358,7 +442,24 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
             }
         }
         const bool issue = kt + RING - 1 < nk;
-        if (issue) stage(pf, kt + RING - 1, std::integral_constant<int, (cur + RING - 1) % RING>{});
+        constexpr bool kSpread = DLLM_EXACT_SPREAD && WREG && !TM && GPS == 1 && !S16;
+        if constexpr (!kSpread) {
+            if (issue) stage(pf, kt + RING - 1, std::integral_constant<int, (cur + RING - 1) % RING>{});
+        }
+        // SPREAD: substep v issues pieces [v kPieces / kSub, (v + 1) kPieces / kSub)
+        auto dma_at = [&](auto v_tag) __attribute__((always_inline)) {
+            if constexpr (kSpread) {
+                constexpr int v = decltype(v_tag)::value, kS = 4 * SPS;
+                constexpr int p0 = v * kPieces / kS, p1 = (v + 1) * kPieces / kS;
+                if (issue) {
+                    [&]<int... Ps>(std::integer_sequence<int, Ps...>) __attribute__((always_inline)) {
+                        (stage_piece(pf, kt + RING - 1, std::integral_constant<int, (cur + RING - 1) % RING>{},
+                                     std::integral_constant<int, p0 + Ps>{}), ...);
+                    }(std::make_integer_sequence<int, p1 - p0>{});
+                }
+            }
+        };
+        DLLM_STAMP_AT(g_stamp_exact, kt <= stamp::kMaxStep ? 2 + 4 * static_cast<int>(kt) : -1);
         if constexpr (!WREG) {
 #pragma unroll
             for (int s = 0; s < SPS; ++s) lds_words<BITS>(w[s], sb + SL::kX + s * SL::kW1 + wave * (64 * BITS * 4), lane);
@@ -459,6 +560,8 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
             // first / last substep of a group (GPS > 1: inside the stage; else the stage's tags)
             constexpr bool gfirst = GPS > 1 ? v % kSubG == 0 : (GF && v == 0);
             constexpr bool glast = GPS > 1 ? v % kSubG == kSubG - 1 : (GL && v == kSub - 1);
+            __builtin_amdgcn_sched_barrier(0);
+            dma_at(v_tag);
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (DLLM_EXACT_PRIO) __builtin_amdgcn_s_setprio(1);
             if constexpr (!HORN && GPS > 1 && glast) read_s4(v / kSubG);
@@ -563,11 +666,14 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
             }(std::make_integer_sequence<int, kSub>{});
         }
         // Stage kt+1 must have landed; (RING 3) kt+2's DMAs may stay in flight across the barrier.
+        DLLM_STAMP_AT(g_stamp_exact, kt <= stamp::kMaxStep ? 3 + 4 * static_cast<int>(kt) : -1);
         if (issue) wait_prev();
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        DLLM_STAMP_AT(g_stamp_exact, kt <= stamp::kMaxStep ? 4 + 4 * static_cast<int>(kt) : -1);
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
+        DLLM_STAMP_AT(g_stamp_exact, kt <= stamp::kMaxStep ? 5 + 4 * static_cast<int>(kt) : -1);
     };
     auto step_tm = [&](const uint8_t *sb, uint8_t *pf, unsigned kt) __attribute__((always_inline)) {
         const bool issue = kt + 2 < nk;
@@ -658,6 +764,7 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
     }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+    DLLM_STAMP_AT(g_stamp_exact, 1);
     for (unsigned kt = 0; kt < nk; kt += kUnroll) {
         [&]<int... Is>(std::integer_sequence<int, Is...>) __attribute__((always_inline)) {
             ((kt + Is < nk ? (at(std::integral_constant<int, Is>{}, kt + Is), 0) : 0), ...);
@@ -715,17 +822,36 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
                         make_float4(acc[r][4 * qd], acc[r][4 * qd + 1], acc[r][4 * qd + 2], acc[r][4 * qd + 3]);
         }
         __syncthreads();
-        if (kg >= 1) return;
+        // coalesced f16 epilogue by all KG NW waves (the image sits past the hand-off area)
+        constexpr bool kCoal = DLLM_EXACT_KG_COAL && std::is_same<YT, __half>::value && !SPLIT && EPI == 0 &&
+                               NW * 64 >= 256 && sizeof(ring) >= (KG - 1) * kXg * 16 + 32 * MR * 64 * NW;
+        const bool coal = kCoal && (m0 + kBMt <= M) && (n0 + kBNt <= N) && (N % 8) == 0;
+        if (kg >= 1 && !coal) return;
+        if (kg == 0) {
 #pragma unroll
-        for (int g = 1; g < KG; ++g)
+            for (int g = 1; g < KG; ++g)
 #pragma unroll
-            for (int r = 0; r < MR; ++r)
+                for (int r = 0; r < MR; ++r)
 #pragma unroll
-                for (int qd = 0; qd < 4; ++qd) {
-                    const float4 o = xch[(g - 1) * kXg + (r * 4 + qd) * 64];
-                    acc[r][4 * qd] += o.x; acc[r][4 * qd + 1] += o.y; acc[r][4 * qd + 2] += o.z; acc[r][4 * qd + 3] += o.w;
-                }
+                    for (int qd = 0; qd < 4; ++qd) {
+                        const float4 o = xch[(g - 1) * kXg + (r * 4 + qd) * 64];
+                        acc[r][4 * qd] += o.x; acc[r][4 * qd + 1] += o.y; acc[r][4 * qd + 2] += o.z; acc[r][4 * qd + 3] += o.w;
+                    }
+        }
+        if constexpr (kCoal) {
+            if (coal) {
+                const int nb0 = n0 + wave * 32 + 4 * hsel;
+                float4 bv[4];
+#pragma unroll
+                for (int qd = 0; qd < 4; ++qd) bv[qd] = *reinterpret_cast<const float4 *>(bias + nb0 + 8 * qd);
+                DLLM_STAMP_AT(g_stamp_exact, stamp::kEpi);
+                store_tile_f16_lds_kg<NW, MR, KG>(ring + (KG - 1) * kXg * 16, acc, bv, reinterpret_cast<__half *>(Y), N, m0,
+                                                  n0, wave, kg, lane);
+                return;
+            }
+        }
     }
+    DLLM_STAMP_AT(g_stamp_exact, stamp::kEpi);
     if constexpr (S16) {
         // element (t, cb, i): m = m0 + 16 t + (lane & 15), n = n0 + 32 wave + 16 cb + 4 rq + i
         const int nc0 = n0 + wave * 32 + 4 * rq;
@@ -998,6 +1124,10 @@ int launch_exact_kpg(const ExactGemmArgs &a, int y_f32, hipStream_t st) {
 }
 
 }  // namespace
+
+#if DLLM_STAMP
+DLLM_STAMP_READER(dllm_stamp_read_exact, g_stamp_exact)
+#endif
 
 bool exact_gemm_supported(int M, int K, int Npad, int group) {
     return M >= 1 && Npad % 128 == 0 && K % group == 0 && (group == 64 || group == 128 || group == 256);
