@@ -207,208 +207,9 @@ __global__ void __launch_bounds__(512) kv_stage_kernel(const uint8_t *__restrict
     for (int i = tid; i < kVImg / 16; i += 512) reinterpret_cast<uint4 *>(dst + kKImg)[i] = sv[i];
 }
 
-#if DLLM_LAB   // lab build only: v4, the unscheduled form of v5 (A/B and ablation masks)
-template <int LAB = 0>
-__global__ void __launch_bounds__(kWaves * 64)
-kv_attention_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__ img, const float *__restrict__ kp,
-                    const float *__restrict__ vp, int S, int H, _Float16 *__restrict__ O) {
-    const int nkb = (S + kKB - 1) / kKB;
-    __shared__ __attribute__((aligned(16))) AttnSmem sm;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int h = blockIdx.y;
-    const int q0 = blockIdx.x * kQT + wave * 32;
-    const int ql = lane & 31, hh = lane >> 5;
-    const float ks = kp[0], vs = vp[0];
-    // exp2 domain, K scale folded in: p = exp2(c * raw - m), c = log2(e) * s_k / sqrt(D).
-    const float c = 1.4426950408889634f * ks / sqrtf(static_cast<float>(kD));
-
-    // Q^T fragments (B operand of S^T = K Q^T): lane holds Q[q = q0 + ql][d = 16 t + 8 hh + j].
-    half8_t qf[kD / 16];
-    {
-        const int qrow = min(q0 + ql, S - 1);
-        const _Float16 *qp = Q + (static_cast<size_t>(qrow) * H + h) * kD + 8 * hh;
-#pragma unroll
-        for (int t = 0; t < kD / 16; ++t) qf[t] = *reinterpret_cast<const half8_t *>(qp + 16 * t);
-    }
-
-    float16_t o[kD / 32];   // O tiles: d-tile dt, lane = d (within tile), rows = query via regs
-#pragma unroll
-    for (int dt = 0; dt < kD / 32; ++dt)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) o[dt][e] = 0.0f;
-    float m_run = -INFINITY, l_run = 0.0f;   // for query q0 + ql (same in both lane halves)
-
-    // S^T (2 x 32 keys x 32 queries) of a staged K block: st[u][r] is key 32u + (r&3) + 8(r>>2) + 4hh
-    // of the block, query q0 + ql.
-    auto qk = [&](float16_t (&st)[2], const _Float16 (&kb_)[kKB][kKRow]) {
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-#pragma unroll
-            for (int e = 0; e < 16; ++e) st[u][e] = 0.0f;
-#pragma unroll
-            for (int t = 0; t < kD / 16; ++t) {
-                const half8_t kf = *reinterpret_cast<const half8_t *>(&kb_[32 * u + ql][16 * t + 8 * hh]);
-                st[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[t], st[u], 0, 0, 0);
-            }
-        }
-    };
-
-    // LDS-DMA of the workspace images: wave w moves pieces w, w + 8, ... (1 KiB each).
-    const uint8_t *himg = img + static_cast<size_t>(h) * nkb * kImg + lane * 16;
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(wave);
-    constexpr bool STAG = false;   // v4: no staggered schedule
-    // pieces p0, p0 + step, ... of an image (the whole workgroup: wv, 8; one group: wv % 4, 4)
-    auto dma_k = [&](int blk, int buf, uint32_t p0 = 0xffffffffu, uint32_t step = kWaves) {
-        const uint8_t *src = himg + static_cast<size_t>(blk) * kImg;
-        const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_addr(&sm.k[buf][0][0]));
-        for (uint32_t p = p0 == 0xffffffffu ? wv : p0; p < kKImg / 1024; p += step) glds16_asm(src + p * 1024, dst + p * 1024);
-    };
-    auto dma_v = [&](int blk, int buf, uint32_t p0 = 0xffffffffu, uint32_t step = kWaves) {
-        const uint8_t *src = himg + static_cast<size_t>(blk) * kImg + kKImg;
-        const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_addr(&sm.vt[buf][0][0]));
-        for (uint32_t p = p0 == 0xffffffffu ? wv : p0; p < kVImg / 1024; p += step) glds16_asm(src + p * 1024, dst + p * 1024);
-    };
-    const bool grp_b = STAG && wave >= kWaves / 2;
-    auto raw_barrier = []() __attribute__((always_inline)) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    // Prologue: K and V of block 0 and K of block 1 staged (STAG: and V of block 1); S^T of block 0.
-    dma_k(0, 0);
-    dma_v(0, 0);
-    if (nkb > 1) dma_k(1, 1);
-    if (STAG && nkb > 1) dma_v(1, 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    float16_t st[2], sn[2];
-    qk(st, sm.k[0]);
-
-    for (int kb = 0; kb < nkb; ++kb) {
-        const int j0 = kb * kKB;
-        const bool more1 = kb + 1 < nkb, more2 = kb + 2 < nkb;
-        // Images in flight during this block's math: K of block kb+2 into the K buffer block kb
-        // used (read last iteration), V of block kb+1 into the V buffer of block kb-1.
-        if (!(LAB & 2)) {
-            if (more2) dma_k(kb + 2, kb & 1);
-            if (more1) dma_v(kb + 1, (kb + 1) & 1);
-        }
-        // S^T of block kb+1 on the matrix pipe while the VALU runs the softmax of block kb.
-        if (more1) {
-            if constexpr (LAB & 8) {
-#pragma unroll
-                for (int u = 0; u < 2; ++u) sn[u] = st[u] * 0.5f;
-            } else {
-                qk(sn, sm.k[(kb + 1) & 1]);
-            }
-        }
-
-        if constexpr (LAB & 1) {   // measurement only: no softmax
-            float lsum = 0.0f;
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) lsum += st[u][r];
-            l_run += lsum;
-        } else {
-        float mloc = -INFINITY;
-        if (__builtin_expect(j0 + kKB > S, 0)) {   // last, partial block only (a real branch)
-            asm volatile("" ::: "memory");
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int key = j0 + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * hh;
-                    st[u][r] = key < S ? st[u][r] : -INFINITY;
-                }
-        }
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) mloc = fmaxf(mloc, st[u][r]);
-        mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-        const float m_new = fmaxf(m_run, mloc * c);
-        // v_exp_f32 directly (exp2f's denormal-range fix-up costs 3-4 extra VALU per element; P
-        // values below 2^-126 are 0 in the f16 P anyway).  exp2(0) = 1 exactly: alpha is exactly 1
-        // when the max did not move.
-        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-        float lsum = 0.0f;
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                st[u][r] = __builtin_amdgcn_exp2f(fmaf(st[u][r], c, -m_new));
-                lsum += st[u][r];
-            }
-        lsum += __shfl_xor(lsum, 32, 64);
-        l_run = l_run * alpha + lsum;
-        m_run = m_new;
-        // ---- rescale O rows by their query's alpha, only if some query's max moved ----
-        if (!__all(alpha == 1.0f)) {
-            if (hh == 0) sm.bcast[wave][ql] = alpha;
-            __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
-            __builtin_amdgcn_wave_barrier();
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const float4 a4 = *reinterpret_cast<const float4 *>(&sm.bcast[wave][8 * g + 4 * hh]);
-#pragma unroll
-                for (int dt = 0; dt < kD / 32; ++dt) {
-                    o[dt][4 * g + 0] *= a4.x; o[dt][4 * g + 1] *= a4.y;
-                    o[dt][4 * g + 2] *= a4.z; o[dt][4 * g + 3] *= a4.w;
-                }
-            }
-        }
-        }
-        // ---- O += P (q_v - z_v): P^T accumulator as the A operand (k-step s: keys 16s..16s+15) ----
-        const auto &vt = sm.vt[kb & 1];
-        if constexpr (!(LAB & 4)) {
-#pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2) {
-            const int u = s2 >> 1, sl = s2 & 1;
-            half8_t pa;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) pa[j] = static_cast<_Float16>(st[u][8 * sl + j]);
-#pragma unroll
-            for (int dt = 0; dt < kD / 32; ++dt) {
-                // element j <-> key 16s + 8(j>>2) + 4hh + (j&3), d = 32dt + ql
-                const _Float16 *vrow = &vt[32 * dt + ql][16 * s2 + 8 * hh];   // kv_pos layout
-                const half4_t lo = *reinterpret_cast<const half4_t *>(vrow);
-                const half4_t hi = *reinterpret_cast<const half4_t *>(vrow + 4);
-                const half8_t vb = half8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(pa, vb, o[dt], 0, 0, 0);
-            }
-        }
-        } else {
-#pragma unroll
-            for (int dt = 0; dt < kD / 32; ++dt) o[dt] += st[dt >> 1] * 0.25f;
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (more1) {
-            st[0] = sn[0];
-            st[1] = sn[1];
-        }
-    }
-
-    // ---- normalise (1/l and the V scale) and store: o[dt][r] -> query q0 + (r&3) + 8(r>>2) + 4hh ----
-    if (hh == 0) sm.bcast[wave][ql] = vs / l_run;
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-        const float4 inv = *reinterpret_cast<const float4 *>(&sm.bcast[wave][8 * g + 4 * hh]);
-        const float iv[4] = {inv.x, inv.y, inv.z, inv.w};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int q = q0 + 8 * g + 4 * hh + i;
-            if (q >= S) continue;
-            _Float16 *op = O + (static_cast<size_t>(q) * H + h) * kD + ql;
-#pragma unroll
-            for (int dt = 0; dt < kD / 32; ++dt) op[32 * dt] = static_cast<_Float16>(o[dt][4 * g + i] * iv[i]);
-        }
-    }
-}
-#endif  // DLLM_LAB
+#if DLLM_LAB   // attention v4 (the unscheduled form of v5; A/B and ablation masks)
+#include "lab/attn_v4.inc"
+#endif
 
 // Row reductions across the two lane halves (lane l and l ^ 32 hold the two key halves of one
 // query): v_permlane32_swap (VALU) instead of a ds_bpermute round trip through the LDS unit.
@@ -762,253 +563,9 @@ kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__
 }
 
 
-#if DLLM_LAB   // lab build only: v6, A/B against v5 (bit-identical, slower: DESIGN.md section 4)
-// v6: one wave per SIMD (4 waves per workgroup, the same 256 queries and LDS ring), each wave
-// owning 64 queries as two 32-query blocks b = 0, 1 with the whole 512-entry register file
-// (__launch_bounds__(256, 1)).  Every K fragment read from LDS feeds the S^T MFMAs of both query
-// blocks and every V fragment both P V MFMAs, so LDS reads per MFMA halve against v5 (one 16-B
-// read per two MFMAs), and the two query blocks give 4 independent accumulator chains in region 1
-// and 8 in region 2.  Same algorithm, block order and per-query arithmetic as v5, so the outputs
-// equal v5's bit for bit.
-constexpr int kW6 = 4;
-constexpr int kQB6 = 2;
-
-struct AttnSmem6 {
-    _Float16 k[2][kKB][kKRow];
-    _Float16 vt[2][kD][kVRow];
-    float bcast[kW6][kQB6][32];
-};
-
-template <int LAB = 0>
-__global__ void __launch_bounds__(kW6 * 64, 1)
-kv_attention6_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__ img, const float *__restrict__ kp,
-                     const float *__restrict__ vp, int S, int H, _Float16 *__restrict__ O) {
-    const int nkb = (S + kKB - 1) / kKB;
-    __shared__ __attribute__((aligned(16))) AttnSmem6 sm;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int h = blockIdx.y;
-    const int qw0 = blockIdx.x * kQT + wave * 32 * kQB6;   // query block b starts at qw0 + 32 b
-    const int ql = lane & 31, hh = lane >> 5;
-    const float ks = kp[0], vs = vp[0];
-    const float c = 1.4426950408889634f * ks / sqrtf(static_cast<float>(kD));
-
-    half8_t qf[kQB6][kD / 16];
-#pragma unroll
-    for (int b = 0; b < kQB6; ++b) {
-        const int qrow = min(qw0 + 32 * b + ql, S - 1);
-        const _Float16 *qp = Q + (static_cast<size_t>(qrow) * H + h) * kD + 8 * hh;
-#pragma unroll
-        for (int t = 0; t < kD / 16; ++t) qf[b][t] = *reinterpret_cast<const half8_t *>(qp + 16 * t);
-    }
-    float16_t o[kQB6][kD / 32];
-#pragma unroll
-    for (int b = 0; b < kQB6; ++b)
-#pragma unroll
-        for (int dt = 0; dt < kD / 32; ++dt)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) o[b][dt][e] = 0.0f;
-    float m_run[kQB6], l_run[kQB6];
-#pragma unroll
-    for (int b = 0; b < kQB6; ++b) { m_run[b] = -INFINITY; l_run[b] = 0.0f; }
-
-    // S^T of a staged K block for both query blocks: st[b][u][r] = key 32u + (r&3) + 8(r>>2) + 4hh.
-    auto qk = [&](float16_t (&st)[kQB6][2], const _Float16 (&kb_)[kKB][kKRow]) {
-#pragma unroll
-        for (int b = 0; b < kQB6; ++b)
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-#pragma unroll
-                for (int e = 0; e < 16; ++e) st[b][u][e] = 0.0f;
-#pragma unroll
-        for (int t = 0; t < kD / 16; ++t)
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const half8_t kf = *reinterpret_cast<const half8_t *>(&kb_[32 * u + ql][16 * t + 8 * hh]);
-#pragma unroll
-                for (int b = 0; b < kQB6; ++b)
-                    st[b][u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[b][t], st[b][u], 0, 0, 0);
-            }
-    };
-
-    const uint8_t *himg = img + static_cast<size_t>(h) * nkb * kImg + lane * 16;
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(wave);
-    auto dma_k = [&](int blk, int buf) {
-        const uint8_t *src = himg + static_cast<size_t>(blk) * kImg;
-        const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_addr(&sm.k[buf][0][0]));
-        for (uint32_t p = wv; p < kKImg / 1024; p += kW6) glds16_asm(src + p * 1024, dst + p * 1024);
-    };
-    auto dma_v = [&](int blk, int buf) {
-        const uint8_t *src = himg + static_cast<size_t>(blk) * kImg + kKImg;
-        const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_addr(&sm.vt[buf][0][0]));
-        for (uint32_t p = wv; p < kVImg / 1024; p += kW6) glds16_asm(src + p * 1024, dst + p * 1024);
-    };
-    dma_k(0, 0);
-    dma_v(0, 0);
-    if (nkb > 1) dma_k(1, 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-
-    auto iter = [&](float16_t (&st)[kQB6][2], float16_t (&sn)[kQB6][2], int kb) {
-        const int j0 = kb * kKB;
-        const bool more1 = kb + 1 < nkb, more2 = kb + 2 < nkb;
-        if constexpr (!(LAB & 2)) {
-            if (more2) dma_k(kb + 2, kb & 1);
-            if (more1) dma_v(kb + 1, (kb + 1) & 1);
-        }
-        if (__builtin_expect(j0 + kKB > S, 0)) {   // last, partial block only
-            asm volatile("" ::: "memory");
-#pragma unroll
-            for (int b = 0; b < kQB6; ++b)
-#pragma unroll
-                for (int u = 0; u < 2; ++u)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int key = j0 + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * hh;
-                        st[b][u][r] = key < S ? st[b][u][r] : -INFINITY;
-                    }
-        }
-        // ---- region 1: S^T of block kb+1 (both query blocks) beside the softmax of block kb ----
-        const auto &kn = sm.k[(kb + 1) & 1];
-#pragma unroll
-        for (int b = 0; b < kQB6; ++b)
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-#pragma unroll
-                for (int e = 0; e < 16; ++e) sn[b][u][e] = 0.0f;
-#pragma unroll
-        for (int t = 0; t < kD / 16; ++t)
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const half8_t kf = *reinterpret_cast<const half8_t *>(&kn[32 * u + ql][16 * t + 8 * hh]);
-#pragma unroll
-                for (int b = 0; b < kQB6; ++b) {
-                    if constexpr (LAB & 8) {
-                        asm volatile("" ::"v"(kf));
-                        sn[b][u][t] += 1.0f;
-                    } else {
-                        sn[b][u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[b][t], sn[b][u], 0, 0, 0);
-                    }
-                }
-            }
-        float alpha[kQB6];
-#pragma unroll
-        for (int b = 0; b < kQB6; ++b) {
-            float mt[16];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) mt[r] = fmaxf(st[b][0][r], st[b][1][r]);
-#pragma unroll
-            for (int w = 8; w >= 1; w >>= 1)
-#pragma unroll
-                for (int r = 0; r < w; ++r) mt[r] = fmaxf(mt[r], mt[r + w]);
-            const float mloc = swap_halves_max(mt[0]);
-            const float m_new = fmaxf(m_run[b], mloc * c);
-            alpha[b] = __builtin_amdgcn_exp2f(m_run[b] - m_new);
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) st[b][u][r] = __builtin_amdgcn_exp2f(fmaf(st[b][u][r], c, -m_new));
-            m_run[b] = m_new;
-        }
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
-#pragma unroll
-        for (int i = 0; i < 32; ++i) {
-            if (i < 14) __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-            __builtin_amdgcn_sched_group_barrier(0x002, 4, 1);
-        }
-        // ---- rescale O rows whose query's max moved (rare after the first blocks) ----
-#pragma unroll
-        for (int b = 0; b < kQB6; ++b) {
-            if (!__all(alpha[b] == 1.0f)) {
-                if (hh == 0) sm.bcast[wave][b][ql] = alpha[b];
-                __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
-                __builtin_amdgcn_wave_barrier();
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const float4 a4 = *reinterpret_cast<const float4 *>(&sm.bcast[wave][b][8 * g + 4 * hh]);
-#pragma unroll
-                    for (int dt = 0; dt < kD / 32; ++dt) {
-                        o[b][dt][4 * g + 0] *= a4.x; o[b][dt][4 * g + 1] *= a4.y;
-                        o[b][dt][4 * g + 2] *= a4.z; o[b][dt][4 * g + 3] *= a4.w;
-                    }
-                }
-            }
-        }
-        // ---- region 2: O += P (q_v - z_v) for both query blocks, one V read per two MFMAs ----
-        const auto &vt = sm.vt[kb & 1];
-#pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2) {
-            const int u = s2 >> 1, sl = s2 & 1;
-            half8_t pa[kQB6];
-#pragma unroll
-            for (int b = 0; b < kQB6; ++b)
-#pragma unroll
-                for (int j = 0; j < 8; ++j) pa[b][j] = static_cast<_Float16>(st[b][u][8 * sl + j]);
-#pragma unroll
-            for (int dt = 0; dt < kD / 32; ++dt) {
-                const half8_t vb = *reinterpret_cast<const half8_t *>(&vt[32 * dt + ql][16 * s2 + 8 * hh]);
-#pragma unroll
-                for (int b = 0; b < kQB6; ++b) {
-                    if constexpr (LAB & 4) {
-                        asm volatile("" ::"v"(vb), "v"(pa[b]));
-                    } else {
-                        o[b][dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(pa[b], vb, o[b][dt], 0, 0, 0);
-                    }
-                }
-            }
-        }
-#pragma unroll
-        for (int b = 0; b < kQB6; ++b) {
-            float ls[16];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) ls[r] = st[b][0][r] + st[b][1][r];
-#pragma unroll
-            for (int w = 8; w >= 1; w >>= 1)
-#pragma unroll
-                for (int r = 0; r < w; ++r) ls[r] = ls[r] + ls[r + w];
-            l_run[b] = l_run[b] * alpha[b] + swap_halves_sum(ls[0]);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 2);
-#pragma unroll
-        for (int i = 0; i < 32; ++i) {
-            if (i < 14) __builtin_amdgcn_sched_group_barrier(0x100, 1, 2);
-            __builtin_amdgcn_sched_group_barrier(0x002, 3, 2);
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    };
-    float16_t sa[kQB6][2], sb[kQB6][2];
-    qk(sa, sm.k[0]);
-    for (int kb = 0; kb < nkb; kb += 2) {
-        iter(sa, sb, kb);
-        if (kb + 1 < nkb) iter(sb, sa, kb + 1);
-    }
-
-    // ---- normalise (1/l and the V scale) and store ----
-#pragma unroll
-    for (int b = 0; b < kQB6; ++b)
-        if (hh == 0) sm.bcast[wave][b][ql] = vs / l_run[b];
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int b = 0; b < kQB6; ++b)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const float4 inv = *reinterpret_cast<const float4 *>(&sm.bcast[wave][b][8 * g + 4 * hh]);
-            const float iv[4] = {inv.x, inv.y, inv.z, inv.w};
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int q = qw0 + 32 * b + 8 * g + 4 * hh + i;
-                if (q >= S) continue;
-                _Float16 *op = O + (static_cast<size_t>(q) * H + h) * kD + ql;
-#pragma unroll
-                for (int dt = 0; dt < kD / 32; ++dt) op[32 * dt] = static_cast<_Float16>(o[b][dt][4 * g + i] * iv[i]);
-            }
-        }
-}
-
-#endif  // DLLM_LAB
+#if DLLM_LAB   // attention v6 (one wave per SIMD; A/B against v5)
+#include "lab/attn_v6.inc"
+#endif
 }  // namespace
 }  // namespace dllm
 

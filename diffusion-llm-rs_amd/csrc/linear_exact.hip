@@ -68,11 +68,6 @@
 #ifndef DLLM_EXACT_KG_COAL
 #define DLLM_EXACT_KG_COAL 1
 #endif
-// DLLM_EXACT_SPREAD = 1 (A/B): the stage's LDS-DMA / weight loads are issued a few per substep (in
-// front of that substep's MFMAs) instead of as one burst at the head of the step.
-#ifndef DLLM_EXACT_SPREAD
-#define DLLM_EXACT_SPREAD 0
-#endif
 
 #include <algorithm>
 #include <type_traits>
@@ -100,6 +95,21 @@ constexpr int kExactMF = 2;
 #else
 #define EXACT_MFMA(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_f16((a), (b), (c), 0, 0, 0)
 constexpr int kExactMF = 1;
+#endif
+// DLLM_EXACT_ABL (stamp / timing builds only, results wrong): 1 = no LDS-DMA or weight loads after
+// the prologue (the MFMA + VALU + LDS-read skeleton); 2 = no MFMAs (operands kept live: the load +
+// VALU skeleton).  Prices the two halves of a k-step in cycles (profiles/r05_shard/).
+#ifndef DLLM_EXACT_ABL
+#define DLLM_EXACT_ABL 0
+#endif
+#if DLLM_EXACT_ABL == 2
+__device__ __forceinline__ float16_t exact_abl_nomfma(const half8_t &a, const half8_t &b, float16_t c) {
+    asm volatile("" ::"v"(a), "v"(b));
+    asm volatile("" : "+v"(c));
+    return c;
+}
+#undef EXACT_MFMA
+#define EXACT_MFMA(a, b, c) exact_abl_nomfma((a), (b), (c))
 #endif
 
 namespace dllm {
@@ -343,26 +353,6 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
         if (has_sz) blds16_asm(prs, poff, goff, u(base + SL::kX + SL::kW + pg * 1024));
         if (has_sf) blds16_asm(prs, poff, goff, u(base + SL::kX + SL::kW + SL::kSZ + pg * 1024));
     };
-    // The same loads one piece at a time (SPREAD): pieces 0 .. SPS kR1 - 1 are X, then the SPS weight
-    // loads, then the group's {zp, scale} words; issue order (hence every vmcnt count) is stage()'s.
-    constexpr int kPieces = SPS * SL::kR1 + SPS + 1;
-    auto stage_piece = [&](uint8_t *sb, unsigned kt, auto slot_tag, auto p_tag) __attribute__((always_inline)) {
-        constexpr int slot = decltype(slot_tag)::value, p = decltype(p_tag)::value;
-        const uint32_t base = u(lds_addr(sb));
-        const unsigned slab0 = (kt + kt0) * SPS;
-        if constexpr (p < SPS * SL::kR1) {
-            constexpr int s = p / SL::kR1, i = p % SL::kR1;
-            blds16_asm(xrs, xoff[i], u((slab0 + s) * kBK * 2), u(base + s * SL::kX1 + wv * 1024 + i * NW * 1024));
-        } else if constexpr (p < SPS * SL::kR1 + SPS) {
-            constexpr int s = p - SPS * SL::kR1;
-            static_assert(WREG, "spread issue: register-staged weight words only");
-            bload16_asm(wq[slot][s], wrs, woff, u((slab0 + s) * 64 * BITS * 4));
-        } else {
-            const uint32_t goff = u((slab0 / spg + pg) * static_cast<uint32_t>(Npad) * 4);
-            if (has_sz) blds16_asm(prs, poff, goff, u(base + SL::kX + SL::kW + pg * 1024));
-            if (has_sf) blds16_asm(prs, poff, goff, u(base + SL::kX + SL::kW + SL::kSZ + pg * 1024));
-        }
-    };
     // Counted wait leaving the newest stage's DMAs (this wave's own count) in flight.
     // (RING > 3: the RING - 2 newest stages stay in flight.)
     static_assert((RING - 2) * (SL::kXRounds + SL::kWOps + 1) <= 63, "vmcnt range");
@@ -441,24 +431,8 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
                 for (int j = 0; j < BITS; ++j) w[s][j] = wq[cur][s][j];
             }
         }
-        const bool issue = kt + RING - 1 < nk;
-        constexpr bool kSpread = DLLM_EXACT_SPREAD && WREG && !TM && GPS == 1 && !S16;
-        if constexpr (!kSpread) {
-            if (issue) stage(pf, kt + RING - 1, std::integral_constant<int, (cur + RING - 1) % RING>{});
-        }
-        // SPREAD: substep v issues pieces [v kPieces / kSub, (v + 1) kPieces / kSub)
-        auto dma_at = [&](auto v_tag) __attribute__((always_inline)) {
-            if constexpr (kSpread) {
-                constexpr int v = decltype(v_tag)::value, kS = 4 * SPS;
-                constexpr int p0 = v * kPieces / kS, p1 = (v + 1) * kPieces / kS;
-                if (issue) {
-                    [&]<int... Ps>(std::integer_sequence<int, Ps...>) __attribute__((always_inline)) {
-                        (stage_piece(pf, kt + RING - 1, std::integral_constant<int, (cur + RING - 1) % RING>{},
-                                     std::integral_constant<int, p0 + Ps>{}), ...);
-                    }(std::make_integer_sequence<int, p1 - p0>{});
-                }
-            }
-        };
+        const bool issue = DLLM_EXACT_ABL != 1 && kt + RING - 1 < nk;
+        if (issue) stage(pf, kt + RING - 1, std::integral_constant<int, (cur + RING - 1) % RING>{});
         DLLM_STAMP_AT(g_stamp_exact, kt <= stamp::kMaxStep ? 2 + 4 * static_cast<int>(kt) : -1);
         if constexpr (!WREG) {
 #pragma unroll
@@ -560,8 +534,6 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
             // first / last substep of a group (GPS > 1: inside the stage; else the stage's tags)
             constexpr bool gfirst = GPS > 1 ? v % kSubG == 0 : (GF && v == 0);
             constexpr bool glast = GPS > 1 ? v % kSubG == kSubG - 1 : (GL && v == kSub - 1);
-            __builtin_amdgcn_sched_barrier(0);
-            dma_at(v_tag);
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (DLLM_EXACT_PRIO) __builtin_amdgcn_s_setprio(1);
             if constexpr (!HORN && GPS > 1 && glast) read_s4(v / kSubG);

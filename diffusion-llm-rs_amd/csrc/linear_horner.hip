@@ -80,352 +80,9 @@ __device__ __forceinline__ void horner_burst(__amdgpu_buffer_rsrc_t xr, uint32_t
 // no DMA at all; bit 7 no MFMA (the DMA ring, waits and barriers alone).  Bit 8 (product): the
 // stage's DMA pieces spread one per MFMA pair over the second half k-step instead of one burst
 // (bit-identical; 124.9 -> 123.6 us at M = 4096 in one process, profiles/r04_horner/).
-template <typename YT, int EPI, int MODE>
-__global__ void __launch_bounds__(512, 1)
-wq_horner_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdev,
-                 const uint32_t *__restrict__ sz, const float *__restrict__ hr, const float *__restrict__ sf,
-                 const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad, int nbm, int nbn,
-                 PSampleEpi epi, int grows = 0) {
-    constexpr bool STAG = MODE & 1;
-    __shared__ __attribute__((aligned(16))) uint8_t smem[3 * kHStage];
-
-    // XCD-aware bijective remap: blocks b and b + 8 share an XCD under round-robin dispatch, so the
-    // 32 tiles an XCD holds at once are consecutive (2 row-blocks x 16 column-blocks at N = 4096).
-    const int nb = nbm * nbn, orig = blockIdx.x;
-    const int xcd = orig % kXCDs, q8 = nb / kXCDs, r8 = nb % kXCDs;
-    const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / kXCDs;
-    int bm = tile / nbn, bn = tile % nbn;
-    if (DLLM_LAB && (grows == 2 || grows == 4 || grows == 8 || grows == 16) && nb == 256 && nbm == 16 && nbn == 16) {
-        // lab A/B: each XCD's 32 tiles as grows row-blocks x (32 / grows) column-blocks (grows in
-        // {2, 4, 8, 16}: 32 / grows must tile the 16 column blocks; every bm, bn stays in 0..15)
-        const int gc = 32 / grows, reg = tile / 32, loc = tile % 32, per_row = 16 / gc;
-        bm = (reg / per_row) * grows + loc / gc;
-        bn = (reg % per_row) * gc + loc % gc;
-    }
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int m0 = bm * 256, n0 = bn * 256;
-    const int nk = K / kBK;   // 64-deep k-steps, even (K % 128 == 0)
-
-    // DMA sources: buffer descriptors at the block's first X row / the wave's weight column tile /
-    // the block's first column of sz and hr, fixed per-lane offsets, the k-step in the SGPR offset.
-    uint32_t xo[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int row = (i * 8 + wave) * 8 + (lane >> 3);
-        const int rrow = (m0 + row < M ? m0 + row : M - 1) - m0;   // rows past M re-read row M - 1
-        const int c = (lane & 7) ^ ((row >> 1) & 7);
-        xo[i] = static_cast<uint32_t>((rrow * K + c * 8) * 2);
-    }
-    const __amdgpu_buffer_rsrc_t xr = raw_rsrc(X + static_cast<size_t>(m0) * K);
-    const uint32_t nt = static_cast<uint32_t>(n0 + 32 * wave) >> 5;
-    const __amdgpu_buffer_rsrc_t wr = raw_rsrc(wdev + static_cast<size_t>(nt) * nk * 64 * 4);
-    const uint32_t wo = static_cast<uint32_t>(lane * 16);
-    // group data: wave 0 stages the {zp, scale} pairs, wave 1 the ratios (256 columns x 4 B each)
-    const __amdgpu_buffer_rsrc_t gr =
-        raw_rsrc(wave == 0 ? static_cast<const void *>(sz + n0) : static_cast<const void *>(hr + n0));
-    const bool has_g = wave < 2;
-    const uint32_t sbase = __builtin_amdgcn_readfirstlane(lds_addr(smem));
-
-    auto stage = [&](int slot, int kt, bool gf) __attribute__((always_inline)) {
-        const uint32_t base = sbase + static_cast<uint32_t>(slot * kHStage);
-        if constexpr ((MODE & 64) != 0) {
-            // lab ablation: no DMA at all
-        } else if constexpr ((MODE & 32) != 0) {   // lab ablation: the weight words only
-            blds16_asm(wr, wo, static_cast<uint32_t>(kt * 1024), base + static_cast<uint32_t>(kHX + wave * 1024));
-        } else {
-            horner_burst(xr, xo[0], xo[1], xo[2], xo[3], static_cast<uint32_t>(kt * kBK * 2), wr, wo,
-                         static_cast<uint32_t>(kt * 1024), base + static_cast<uint32_t>(wave * 1024));
-        }
-        if ((MODE & 64) == 0 && gf && has_g)
-            blds16_asm(gr, wo, static_cast<uint32_t>((kt >> 1) * Npad * 4),
-                       base + static_cast<uint32_t>(kHX + kHW + wave * 1024));
-    };
-
-    float16_t acc[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[r][e] = 0.0f;
-
-    const int hsel = lane >> 5;
-    const int rowx = ((lane & 31) >> 1) & 7;
-    int soff[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) soff[s] = (lane & 31) * (kBK * 2) + ((((2 * s + hsel) ^ rowx)) << 4);
-
-    auto read_b = [&](half8_t (&b)[8], const uint8_t *sb, int s) __attribute__((always_inline)) {
-#pragma unroll
-        for (int r = 0; r < 8; ++r) b[r] = *reinterpret_cast<const half8_t *>(sb + soff[s] + r * 32 * kBK * 2);
-    };
-
-    ExactConsts ec;
-    uint32_t w[4];
-    float4 r4[4];
-    half8_t bA[8], bB[8], aA, aB;
-    // MODE bit 9 (lab ablation, results wrong, timing only): each 32x32x16 MFMA replaced by two
-    // 16x16x32 MFMAs on the same operands (equal FLOPs; the MFMA shape's effect on the held clock)
-    constexpr int kMF = (MODE & 512) ? 2 : 1;
-    typedef float fx4 __attribute__((ext_vector_type(4)));
-    typedef float fx8 __attribute__((ext_vector_type(8)));
-    auto mm = [&](const half8_t &a, const half8_t &b, float16_t &c) __attribute__((always_inline)) {
-        if constexpr ((MODE & 512) != 0) {
-            fx4 c0 = __builtin_shufflevector(c, c, 0, 1, 2, 3);
-            fx4 c1 = __builtin_shufflevector(c, c, 4, 5, 6, 7);
-            c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c0, 0, 0, 0);
-            c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c1, 0, 0, 0);
-            const fx8 lo = __builtin_shufflevector(c0, c1, 0, 1, 2, 3, 4, 5, 6, 7);
-            const fx8 hi = __builtin_shufflevector(c, c, 8, 9, 10, 11, 12, 13, 14, 15);
-            c = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
-        } else {
-            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
-        }
-    };
-    // MODE bit 8: the pending stage's pieces, issued between MFMA pairs of substeps 2 and 3
-    int pend_slot = 0, pend_kt = 0;
-    bool pend_gf = false, pend_on = false;
-    auto piece = [&](int p) __attribute__((always_inline)) {
-        if (!pend_on) return;
-        const uint32_t base = sbase + static_cast<uint32_t>(pend_slot * kHStage);
-        if (p < 4)
-            blds16_asm(xr, xo[p], static_cast<uint32_t>(pend_kt * kBK * 2),
-                       base + static_cast<uint32_t>(wave * 1024 + p * 0x2000));
-        else if (p == 4)
-            blds16_asm(wr, wo, static_cast<uint32_t>(pend_kt * 1024), base + static_cast<uint32_t>(kHX + wave * 1024));
-        else if (pend_gf && has_g)
-            blds16_asm(gr, wo, static_cast<uint32_t>((pend_kt >> 1) * Npad * 4),
-                       base + static_cast<uint32_t>(kHX + kHW + wave * 1024));
-    };
-    auto sub = [&](const uint8_t *sb, half8_t (&bc)[8], half8_t (&bn)[8], const half8_t &ac, half8_t &an, int j,
-                   bool gf) __attribute__((always_inline)) {
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
-        if constexpr ((MODE & 256) != 0) {
-            if (j >= 2) {
-                // quarters of 2 MFMAs, each with its share of the next substep's B reads and
-                // dequant, and a DMA piece between quarters
-                if (j < 3) {
-                    if constexpr ((MODE & 8) != 0) an = ac;   // lab ablation: one dequant per k-step
-                    else an = dequant_exact<4>(w, j + 1, ec);
-                }
-                const half8_t (&bq)[8] = (MODE & 16) ? bA : bc;   // lab ablation: one B read per k-step
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    if ((MODE & 16) == 0 && j < 3) {
-                        bn[2 * q] = *reinterpret_cast<const half8_t *>(sb + soff[j + 1] + (2 * q) * 32 * kBK * 2);
-                        bn[2 * q + 1] = *reinterpret_cast<const half8_t *>(sb + soff[j + 1] + (2 * q + 1) * 32 * kBK * 2);
-                    }
-                    mm(ac, bq[2 * q], acc[2 * q]);
-                    mm(ac, bq[2 * q + 1], acc[2 * q + 1]);
-                    __builtin_amdgcn_sched_group_barrier(0x008, kMF, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x008, kMF, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-                    __builtin_amdgcn_sched_barrier(0);
-                    if (q < 3) piece(3 * (j - 2) + q);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-                __builtin_amdgcn_s_setprio(0);
-                __builtin_amdgcn_sched_barrier(0);
-                return;
-            }
-        }
-        if (j < 3) {
-            if constexpr ((MODE & 16) == 0) read_b(bn, sb, j + 1);
-            if constexpr ((MODE & 8) != 0) an = ac;
-            else an = dequant_exact<4>(w, j + 1, ec);
-        }
-        const half8_t (&bu)[8] = (MODE & 16) ? bA : bc;
-        if ((MODE & 4) == 0 && gf && j == 0) {
-            // acc <- acc * r_g right before the group's first MFMA of each rep (scalar v_mul_f32:
-            // the file is built without the SLP vectorizer)
-#pragma unroll
-            for (int r = 0; r < 8; ++r) {
-#pragma unroll
-                for (int qd = 0; qd < 4; ++qd) {
-                    acc[r][4 * qd + 0] *= r4[qd].x;
-                    acc[r][4 * qd + 1] *= r4[qd].y;
-                    acc[r][4 * qd + 2] *= r4[qd].z;
-                    acc[r][4 * qd + 3] *= r4[qd].w;
-                }
-                if constexpr ((MODE & 128) == 0) mm(ac, bu[r], acc[r]);
-            }
-            // rep i + 1's rescale issues beside rep i's MFMA
-            __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                if (i + 1 < 8) __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, kMF, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
-            }
-        } else {
-#pragma unroll
-            for (int r = 0; r < 8; ++r)
-                if constexpr ((MODE & 128) == 0) mm(ac, bu[r], acc[r]);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, kMF, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-            }
-        }
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    auto barrier = []() __attribute__((always_inline)) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    // STAG (the default): waves 4-7 (the second of each SIMD's two waves) run half a k-step behind
-    // waves 0-3 -- one barrier per half k-step, group B entering through one extra barrier -- so a
-    // SIMD's two waves do not reach their LDS read bursts, dequant / rescale VALU and barrier waits
-    // together (MI355X_MICROARCH.md, two waves per SIMD, item 9).  Ring safety: stage kt + 2 is
-    // issued in the second half of k-step kt, after the barrier behind which the lagging group
-    // finished reading slot (kt - 1) % 3; a wave of group A waits for its stage kt + 1 DMAs at the
-    // end of that half (they were issued a half k-step earlier than group B's), a wave of group B at
-    // the end of the first half of k-step kt + 1 (vmcnt 0), in both cases before the barrier behind
-    // which the first wave reads stage kt + 1.
-    const bool grp_b = STAG && wave >= 4;
-    // One k-step on ring slot `slot` (k-step kt); slot (kt + 2) % 3 receives k-step kt + 2.
-    auto step = [&](int slot, int kt, auto gf_tag) __attribute__((always_inline)) {
-        constexpr bool GF = decltype(gf_tag)::value;
-        const bool issue = kt + 2 < nk;
-        if (!STAG && issue) stage((slot + 2) % 3, kt + 2, GF);   // kt + 2 opens a group iff kt does
-        const uint8_t *sb = smem + slot * kHStage;
-        {
-            const uint4 v = *reinterpret_cast<const uint4 *>(sb + kHX + wave * 1024 + lane * 16);
-            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
-        }
-        if constexpr (GF) {
-            half2_t nz, sc;
-            split_sz(*reinterpret_cast<const uint32_t *>(sb + kHX + kHW + (wave * 32 + (lane & 31)) * 4), nz, sc);
-            ec = exact_consts(nz);
-            const float *rl = reinterpret_cast<const float *>(sb + kHX + kHW + 1024) + wave * 32 + 4 * hsel;
-#pragma unroll
-            for (int qd = 0; qd < 4; ++qd) r4[qd] = *reinterpret_cast<const float4 *>(rl + 8 * qd);
-        }
-        read_b(bA, sb, 0);
-        aA = dequant_exact<4>(w, 0, ec);
-        sub(sb, bA, bB, aA, aB, 0, GF);
-        sub(sb, bB, bA, aB, aA, 1, GF);
-        if constexpr (STAG) {
-            if (grp_b) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            barrier();
-            if constexpr ((MODE & 256) != 0) {   // pieces issued inside substeps 2 and 3
-                pend_on = issue;
-                pend_slot = (slot + 2) % 3;
-                pend_kt = kt + 2;
-                pend_gf = GF;
-            } else if (issue) {
-                stage((slot + 2) % 3, kt + 2, GF);
-            }
-        }
-        sub(sb, bA, bB, aA, aB, 2, GF);
-        sub(sb, bB, bA, aB, aA, 3, GF);
-        // k-step kt + 1 must have landed; kt + 2's DMAs stay in flight across the barrier
-        if (!grp_b) {
-            if (issue) {
-                if (GF && has_g) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-                else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-        }
-        barrier();
-    };
-
-    stage(0, 0, true);
-    stage(1, 1, false);
-    asm volatile("s_waitcnt vmcnt(5)" ::: "memory");   // stage 0 landed (stage 1's 5 DMAs in flight)
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (grp_b) barrier();   // group B enters half a k-step behind
-    using GFt = std::integral_constant<bool, true>;
-    using GFf = std::integral_constant<bool, false>;
-    // group = 2 k-steps, ring period 3: unroll 6 so each step's slot and group phase are static
-    for (int kt = 0; kt < nk; kt += 6) {
-        step(0, kt, GFt{});
-        step(1, kt + 1, GFf{});
-        if (kt + 2 < nk) {
-            step(2, kt + 2, GFt{});
-            step(0, kt + 3, GFf{});
-        }
-        if (kt + 4 < nk) {
-            step(1, kt + 4, GFt{});
-            step(2, kt + 5, GFf{});
-        }
-    }
-    if (STAG && !grp_b) barrier();   // group A joins group B's last barrier
-
-    // acc = sum_g T_g s_g / s_{G-1}: times the last group's scales, then the bias
-    const int nb0 = n0 + wave * 32 + 4 * hsel;
-    const float *sl = sf + static_cast<size_t>(nk / 2 - 1) * Npad + nb0;
-    float4 bv[4];
-#pragma unroll
-    for (int qd = 0; qd < 4; ++qd) {
-        const float4 s = *reinterpret_cast<const float4 *>(sl + 8 * qd);
-        bv[qd] = *reinterpret_cast<const float4 *>(bias + nb0 + 8 * qd);
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            acc[r][4 * qd + 0] *= s.x;
-            acc[r][4 * qd + 1] *= s.y;
-            acc[r][4 * qd + 2] *= s.z;
-            acc[r][4 * qd + 3] *= s.w;
-        }
-    }
-    if constexpr ((MODE & 2) != 0) {   // lab ablation: keep the results live, store nothing
-#pragma unroll
-        for (int r = 0; r < 8; ++r) asm volatile("" ::"v"(acc[r]));
-        return;
-    }
-    if constexpr (EPI == 1) {
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            const int m = m0 + r * 32 + (lane & 31);
-            if (m >= M) continue;
-#pragma unroll
-            for (int qd = 0; qd < 4; ++qd) {
-                if (nb0 + 8 * qd >= N) continue;
-                psample4(epi, m, nb0 + 8 * qd, N, acc[r][4 * qd + 0] + bv[qd].x, acc[r][4 * qd + 1] + bv[qd].y,
-                         acc[r][4 * qd + 2] + bv[qd].z, acc[r][4 * qd + 3] + bv[qd].w);
-            }
-        }
-        return;
-    }
-    const bool full = (m0 + 256 <= M) && (n0 + 256 <= N) && (N % 4) == 0;
-    if constexpr (std::is_same<YT, __half>::value) {
-        if (full && (N % 8) == 0) {   // coalesced 16-B row stores (16-B aligned rows) through the drained ring (2 passes of 128 rows)
-            store_tile_f16_lds<8, 8>(smem, 3 * kHStage, acc, bv, Y, N, m0, n0, wave, lane);
-            return;
-        }
-    }
-    if (full) {
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            YT *yrow = Y + static_cast<size_t>(m0 + r * 32 + (lane & 31)) * N + nb0;
-#pragma unroll
-            for (int qd = 0; qd < 4; ++qd)
-                store4<YT>(yrow + 8 * qd, acc[r][4 * qd + 0] + bv[qd].x, acc[r][4 * qd + 1] + bv[qd].y,
-                           acc[r][4 * qd + 2] + bv[qd].z, acc[r][4 * qd + 3] + bv[qd].w);
-        }
-    } else {
-        const bool vec_ok = (N % 4) == 0;
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            const int m = m0 + r * 32 + (lane & 31);
-            if (m >= M) continue;
-            YT *yrow = Y + static_cast<size_t>(m) * N;
-#pragma unroll
-            for (int qd = 0; qd < 4; ++qd)
-                store_out4<YT>(yrow, bias, nb0 + 8 * qd, N, vec_ok, acc[r][4 * qd + 0], acc[r][4 * qd + 1],
-                               acc[r][4 * qd + 2], acc[r][4 * qd + 3]);
-        }
-    }
-}
+#if DLLM_LAB   // the round-3 kernel (32x32x16 MFMAs), lab variant 321 and the ablation harness
+#include "lab/horner_r3.inc"
+#endif
 
 // ---------------------------------------------------------------------------------------------
 // KG2 Horner GEMM: 256-token x 128-column tiles for grids where 256 x 256 tiles leave CUs idle
@@ -835,7 +492,7 @@ __global__ void __launch_bounds__(512, 1)
 wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdev,
                    const uint32_t *__restrict__ sz, const float *__restrict__ hr, const float *__restrict__ sf,
                    const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad, int nbm, int nbn,
-                   PSampleEpi epi, int grows = 0) {
+                   PSampleEpi epi) {
     constexpr bool STAG = MODE & 1;
     using L = H16<TB>;
     constexpr int kStage = L::kStage, kXB = L::kXB, kKPS = L::kKPS;
@@ -845,13 +502,7 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
     const int nb = nbm * nbn, orig = blockIdx.x;
     const int xcd = orig % kXCDs, q8 = nb / kXCDs, r8 = nb % kXCDs;
     const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / kXCDs;
-    int bm = tile / nbn, bn = tile % nbn;
-    if (DLLM_LAB && (grows == 2 || grows == 4 || grows == 8 || grows == 16) && nb == 256 && nbm == 16 && nbn == 16) {
-        // lab A/B: each XCD's 32 tiles as grows row-blocks x (32 / grows) column-blocks
-        const int gc = 32 / grows, reg = tile / 32, loc = tile % 32, per_row = 16 / gc;
-        bm = (reg / per_row) * grows + loc / gc;
-        bn = (reg % per_row) * gc + loc % gc;
-    }
+    const int bm = tile / nbn, bn = tile % nbn;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int m0 = bm * 16 * TB, n0 = bn * 256;
@@ -1224,37 +875,19 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
 }
 
 template <int MODE, int TB = 16>
-void launch_horner16_t(const HornerGemmArgs &a, int y_f32, hipStream_t st, int grows = 0) {
+void launch_horner16_t(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
     const int nbm = (a.M + 16 * TB - 1) / (16 * TB), nbn = a.Npad / 256;
     const unsigned nb = static_cast<unsigned>(nbm * nbn);
     const PSampleEpi ep = a.epi ? *a.epi : PSampleEpi{};
     if (a.epi)
         wq_horner16_kernel<float, 1, MODE, TB><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
-                                                               a.epi->x_prev, a.N, a.Npad, nbm, nbn, ep, grows);
+                                                               a.epi->x_prev, a.N, a.Npad, nbm, nbn, ep);
     else if (y_f32)
         wq_horner16_kernel<float, 0, MODE, TB><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
-                                                               static_cast<float *>(a.Y), a.N, a.Npad, nbm, nbn, ep, grows);
+                                                               static_cast<float *>(a.Y), a.N, a.Npad, nbm, nbn, ep);
     else
         wq_horner16_kernel<__half, 0, MODE, TB><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
-                                                                static_cast<__half *>(a.Y), a.N, a.Npad, nbm, nbn, ep, grows);
-}
-
-template <int MODE>
-void launch_horner_t(const HornerGemmArgs &a, int y_f32, hipStream_t st, int grows = 0) {
-    const int nbm = (a.M + 255) / 256, nbn = a.Npad / 256;
-    const unsigned nb = static_cast<unsigned>(nbm * nbn);
-    const PSampleEpi ep = a.epi ? *a.epi : PSampleEpi{};
-    if (a.epi)
-        wq_horner_kernel<float, 1, MODE><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
-                                                             a.epi->x_prev, a.N, a.Npad, nbm, nbn, ep, grows);
-    else if (y_f32)
-        wq_horner_kernel<float, 0, MODE><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
-                                                             static_cast<float *>(a.Y), a.N, a.Npad, nbm, nbn, ep,
-                                                             grows);
-    else
-        wq_horner_kernel<__half, 0, MODE><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
-                                                              static_cast<__half *>(a.Y), a.N, a.Npad, nbm, nbn, ep,
-                                                              grows);
+                                                                static_cast<__half *>(a.Y), a.N, a.Npad, nbm, nbn, ep);
 }
 
 }  // namespace
@@ -1276,88 +909,13 @@ int launch_horner_kg2_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
     return DLLM_OK;
 }
 
-#if DLLM_LAB
-int launch_horner_rows_gemm(const HornerGemmArgs &a, int rows, int y_f32, hipStream_t st) {
-    if (rows != 128) return fail(DLLM_ERR_INVALID_PARAMS, "Horner tiles: 128 rows");
-    launch_horner16_t<1 | 256, 8>(a, y_f32, st);
-    DLLM_LAUNCH_CHECK();
-    return DLLM_OK;
-}
+#if DLLM_LAB   // launchers and A/B dispatch of the lab Horner variants
+#include "lab/horner_lab_launch.inc"
 #endif
 
 int launch_horner_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
 #if DLLM_LAB
-    if (a.lab == 28) {   // lab A/B: the 16x16x32 kernel with 4 x 8 XCD tile groups
-        launch_horner16_t<1 | 256 | 1024>(a, y_f32, st, 4);
-        DLLM_LAUNCH_CHECK();
-        return DLLM_OK;
-    }
-    if (a.lab == 26 || a.lab == 27) {   // lab A/B: the 16x16x32 kernel without the stagger (26) /
-                                        // with one DMA burst per stage instead of spread pieces (27)
-        if (a.lab == 26) launch_horner16_t<256 | 1024>(a, y_f32, st);
-        else launch_horner16_t<1 | 1024>(a, y_f32, st);
-        DLLM_LAUNCH_CHECK();
-        return DLLM_OK;
-    }
-    if (a.lab == 25) {   // lab A/B: the 16x16x32 kernel with MODE bit 11 (2 % slower on one box:
-                         // profiles/r04_horner/h16_early_dequant_ab.json)
-        launch_horner16_t<1 | 256 | 1024 | 2048>(a, y_f32, st);
-        DLLM_LAUNCH_CHECK();
-        return DLLM_OK;
-    }
-    if (a.lab == 24) {   // lab A/B: the 16x16x32 kernel with half 1's A fragments built at substep 2
-        launch_horner16_t<1 | 256>(a, y_f32, st);
-        DLLM_LAUNCH_CHECK();
-        return DLLM_OK;
-    }
-    if (a.lab == 21) {   // lab A/B: the round-3 MFMA shape (32x32x16) with the product schedule
-        launch_horner_t<1 | 256>(a, y_f32, st);
-        DLLM_LAUNCH_CHECK();
-        return DLLM_OK;
-    }
-    if (a.lab == 19 || a.lab == 20) {   // lab ablations: the MFMA shape (MODE bit 9) in the product
-        // schedule (19) and in the MFMAs-only skeleton of 14 (20)
-        if (a.lab == 19) launch_horner_t<1 | 256 | 512>(a, y_f32, st);
-        else launch_horner_t<3 | 4 | 8 | 16 | 64 | 512>(a, y_f32, st);
-        return DLLM_OK;
-    }
-    if (a.lab == 17 || a.lab == 18) {   // lab ablations: 17 = 305's (no stores, rescale; one dequant and
-                                        // B read) with only the weight-word DMA; 18 = 305's with the spread DMA
-        if (a.lab == 17) launch_horner_t<3 | 4 | 8 | 16 | 32>(a, y_f32, st);
-        else launch_horner_t<3 | 4 | 8 | 16 | 256>(a, y_f32, st);
-        DLLM_LAUNCH_CHECK();
-        return DLLM_OK;
-    }
-    if (a.lab == 16) {   // lab A/B: the round-3 schedule (one DMA burst per stage, no MODE bit 8)
-        launch_horner_t<1>(a, y_f32, st);
-        DLLM_LAUNCH_CHECK();
-        return DLLM_OK;
-    }
-    if (a.lab == 14 || a.lab == 15) {   // lab ablations: MFMAs + barriers only (no DMA, rescale, stores;
-                                        // 1 dequant / B read); 15: the DMA ring + barriers only (no MFMA)
-        if (a.lab == 14) launch_horner_t<3 | 4 | 8 | 16 | 64>(a, y_f32, st);
-        else launch_horner_t<3 | 4 | 8 | 16 | 128>(a, y_f32, st);
-        DLLM_LAUNCH_CHECK();
-        return DLLM_OK;
-    }
-    if (a.lab >= 10 && a.lab <= 12) {   // lab A/B: XCD tile groups 4 x 8 / 8 x 4 / 16 x 2
-        launch_horner_t<1 | 256>(a, y_f32, st, a.lab == 10 ? 4 : a.lab == 11 ? 8 : 16);
-        DLLM_LAUNCH_CHECK();
-        return DLLM_OK;
-    }
-    if (a.lab >= 1 && a.lab <= 9) {   // lab A/B: 1 no stagger; 2.. ablations (see MODE)
-        if (a.lab == 1) launch_horner_t<0>(a, y_f32, st);
-        else if (a.lab == 2) launch_horner_t<3>(a, y_f32, st);
-        else if (a.lab == 3) launch_horner_t<2>(a, y_f32, st);
-        else if (a.lab == 4) launch_horner_t<3 | 4>(a, y_f32, st);
-        else if (a.lab == 5) launch_horner_t<3 | 8>(a, y_f32, st);
-        else if (a.lab == 6) launch_horner_t<3 | 16>(a, y_f32, st);
-        else if (a.lab == 7) launch_horner_t<3 | 4 | 8 | 16>(a, y_f32, st);
-        else if (a.lab == 8) launch_horner_t<3 | 32>(a, y_f32, st);
-        else launch_horner_t<3 | 64>(a, y_f32, st);
-        DLLM_LAUNCH_CHECK();
-        return DLLM_OK;
-    }
+    if (a.lab) return launch_horner_lab(a, y_f32, st);
 #endif
     launch_horner16_t<1 | 256 | 1024>(a, y_f32, st);
     DLLM_LAUNCH_CHECK();

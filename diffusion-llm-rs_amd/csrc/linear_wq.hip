@@ -215,38 +215,9 @@ __global__ void __launch_bounds__(256) build_fragments_kernel(const uint32_t *__
     }
 }
 
-#if DLLM_LAB   // lab build only
-// Canonical -> 16x16x32 prefill layout: [32-column tile][k64 slab][lane][bits words], lane l,
-// "substep" S' = 2 f + s (f: 16-column half of the tile, s: 32-deep half of the slab), code j of
-// the lane's 8 = column 32 nt + 16 f + (l & 15), k = 64 slab + 32 s + 8 (l >> 4) + j; words and
-// pair positions as the 32x32x16 layout with S' in place of its substep.  One thread per (n, slab).
-__global__ void __launch_bounds__(256) build_fragments16_kernel(const uint32_t *__restrict__ canon, size_t K, size_t N,
-                                                                size_t Npad, int bits, uint32_t *__restrict__ w16) {
-    const size_t n = blockIdx.x * static_cast<size_t>(256) + threadIdx.x;
-    const size_t kt = blockIdx.y;
-    if (n >= Npad) return;
-    const size_t nk = K / 64, nt = n >> 5;
-    const int f = static_cast<int>((n >> 4) & 1);
-    const int ppw = 16 / bits;
-    for (int o = 0; o < 4; ++o) {
-        const size_t lane = (n & 15) + 16 * o;
-        uint32_t *dst = w16 + ((nt * nk + kt) * 64 + lane) * bits;
-        uint32_t words[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (int s2 = 0; s2 < 2; ++s2) {
-            for (int v = 0; v < 4; ++v) {
-                const int P = (2 * f + s2) * 4 + v;
-                const size_t k = kt * 64 + 32 * s2 + 8 * o + 2 * v;
-                uint32_t lo = 0, hi = 0;
-                if (n < N) { lo = canon_code(canon, k, n, N, bits); hi = canon_code(canon, k + 1, n, N, bits); }
-                words[P / ppw] |= (lo << (bits * (P % ppw))) | (hi << (16 + bits * (P % ppw)));
-            }
-        }
-        // This thread owns exactly the words of S' = 2f, 2f+1: [8f / ppw, (8f + 8) / ppw).
-        for (int w = (8 * f) / ppw; w < (8 * f + 8) / ppw; ++w) dst[w] = words[w];
-    }
-}
-
-#endif  // DLLM_LAB
+#if DLLM_LAB   // the 16x16x32 prefill weight layout (lab variants 8, 11)
+#include "lab/wq_fragments16.inc"
+#endif
 
 // Code (k, n) from the fragment-major (prefill) layout: lane (n & 31) + 32 ((k % 16) / 8) of the
 // (n / 32, k / 64) slab, pair P = 4 ((k % 64) / 16) + (k % 8) / 2, bit bits (P % (16/bits)) + 16 (k & 1).
@@ -423,233 +394,9 @@ __device__ __forceinline__ void load_words(uint32_t (&w)[BITS], const uint32_t *
     }
 }
 
-#if DLLM_LAB   // lab build only
-// ---------------------------------------------------------------------------------------------
-// Prefill GEMM (M > decode threshold): Y[M][N] = X[M][K] (f16) . W^[K][N] + b, computed as
-// Y^T = W^^T X^T so that the accumulator's lane index is the token m and 4 consecutive
-// registers hold 4 consecutive output columns n (one 8/16-byte store each).
-//   block tile 256 (m) x 128 (n), 4 waves side by side in n, wave tile 256 (m) x 32 (n):
-//   acc[8 m-reps] of 32x32 f32 = 128 VGPRs.  Each wave dequantizes only its own 32 columns
-//   (no redundant dequant; 2.5 VALU per MFMA) and all 4 waves share the X tile.
-//   X tile [256][64] f16 in LDS (2 stages, 64 KiB -> 2 blocks per CU), filled by
-//   global_load_lds 16 B/lane with the 16-B chunk index XOR-swizzled by (row>>1)&7
-//   (conflict-free ds_read_b128 fragments, measured SQ_LDS_BANK_CONFLICT = 0).
-//   W fragments stream straight to VGPRs, one coalesced dwordx4 per lane per 64-deep slab
-//   (int4), one slab ahead.
-// ---------------------------------------------------------------------------------------------
-// LDS stage layout (bytes): X tile [256][64] f16 (32 KiB) | W slabs [4 waves][64 lanes][BITS words]
-// | sz [4 waves][64 lanes] u32.  Everything arrives by global_load_lds, so hipcc's counters see no
-// register-destination global load in the loop (mixing the two kinds makes it wait vmcnt(0) at
-// the first use of a register load, which serialised prefetch and compute in the first version).
-template <int BITS, int MR = kMReps>
-struct StageLayout {
-    static constexpr int kX = 32 * MR * kBK * 2;
-    static constexpr int kW = 4 * 64 * BITS * 4;
-    static constexpr int kSZ = 4 * 64 * 4;
-    static constexpr int kBytes = kX + kW + kSZ;
-};
-
-template <int BITS>
-__device__ __forceinline__ void glds_words(const uint32_t *gsrc, uint8_t *ldst) {
-    // One lane-linear LDS-DMA of BITS*4 bytes per lane (16 B for int4; 8 B as two dwords for int2).
-    if constexpr (BITS == 4) {
-        glds16(gsrc, ldst);
-    } else if constexpr (BITS == 8) {
-        glds16(gsrc, ldst);
-        glds16(gsrc + 4, ldst + 64 * 16);
-    } else {
-        __builtin_amdgcn_global_load_lds((gbl_void_ptr)(const_cast<uint32_t *>(gsrc)), (lds_void_ptr)(ldst), 4, 0, 0);
-        __builtin_amdgcn_global_load_lds((gbl_void_ptr)(const_cast<uint32_t *>(gsrc + 1)), (lds_void_ptr)(ldst + 256),
-                                         4, 0, 0);
-    }
-}
-
-// MR: 32-row m-reps per wave (block tile 32*MR x 128).  SPLIT: the block covers K-slice ks of
-// nsplit and writes its fp32 partial tile to ws[ks][M][Npad] (no bias); splitk_reduce_kernel sums
-// the slices in slice order and applies the bias (deterministic, no atomics).
-template <int BITS, typename YT, int VAR, int MR = kMReps, bool SPLIT = false>
-__global__ void __launch_bounds__(kThreads, (BITS == 8 && MR == 8) ? 1 : 2)
-wq_gemm_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdev,
-               const uint32_t *__restrict__ sz, const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad,
-               int group, int nbm, int nbn, int nsplit = 1, float *__restrict__ ws = nullptr) {
-    using SL = StageLayout<BITS, MR>;
-    constexpr int kBMt = 32 * MR;
-    // Two stage arrays (not one array indexed at run time): with distinct objects the compiler
-    // can prove the LDS-DMA into one stage does not alias the ds_reads of the other, and does not
-    // insert a vmcnt(0) before every fragment read.
-    __shared__ __attribute__((aligned(16))) uint8_t smem0[SL::kBytes];
-    __shared__ __attribute__((aligned(16))) uint8_t smem1[SL::kBytes];
-
-    // XCD-aware bijective remap: consecutive logical tiles (same bm row panel of X) share an XCD.
-    // K-slice outermost, so the blocks an XCD holds share the slice's X rows in its L2.
-    const int nb = nbm * nbn * nsplit, orig = blockIdx.x;
-    const int xcd = orig % kXCDs, q8 = nb / kXCDs, r8 = nb % kXCDs;
-    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / kXCDs;
-    const int ks = wgid / (nbm * nbn), tile = wgid % (nbm * nbn);
-    const int bm = tile / nbn, bn = tile % nbn;
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int m0 = bm * kBMt, n0 = bn * kBN;
-    const unsigned nk_all = static_cast<unsigned>(K) / kBK;
-    const unsigned nk = nk_all / static_cast<unsigned>(nsplit);   // k-steps in this slice
-    const unsigned kt0 = static_cast<unsigned>(ks) * nk;
-    const unsigned kpg = static_cast<unsigned>(group) / kBK;   // k-steps per quantization group
-    const unsigned nt = static_cast<unsigned>(n0 + wave * 32) >> 5;
-    const int ncol = n0 + wave * 32 + (lane & 31);
-
-    // glds source pointers.
-    const int chunk_st = lane & 7;
-    const __half *xsrc[MR];
-#pragma unroll
-    for (int i = 0; i < MR; ++i) {
-        const int row = i * 32 + wave * 8 + (lane >> 3);
-        int grow = m0 + row;
-        grow = grow < M ? grow : M - 1;
-        const int c = chunk_st ^ ((row >> 1) & 7);
-        xsrc[i] = X + static_cast<size_t>(grow) * K + c * 8;
-    }
-    const uint32_t *wsrc = wdev + (static_cast<size_t>(nt) * nk_all * 64 + lane) * BITS;   // + kt*64*BITS
-    const uint32_t *szsrc = sz + ncol;                                                  // + g*Npad
-
-    auto stage = [&](uint8_t *sb, unsigned kt) {
-        uint8_t *xb = sb + wave * 1024;   // 1 KiB per wave-instruction
-        kt += kt0;
-#pragma unroll
-        for (int i = 0; i < MR; ++i) glds16(xsrc[i] + kt * kBK, xb + i * 4096);
-        glds_words<BITS>(wsrc + static_cast<size_t>(kt) * 64 * BITS, sb + SL::kX + wave * (64 * BITS * 4));
-        __builtin_amdgcn_global_load_lds((gbl_void_ptr)(const_cast<uint32_t *>(szsrc + (kt / kpg) * Npad)),
-                                         (lds_void_ptr)(sb + SL::kX + SL::kW + wave * 256), 4, 0, 0);
-    };
-
-    float16_t acc[MR];
-#pragma unroll
-    for (int r = 0; r < MR; ++r)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[r][e] = 0.0f;
-
-    // LDS fragment offsets (bytes): row = 32r + (lane&31); (row>>1)&7 does not depend on r.
-    const int hsel = lane >> 5;
-    const int rowx = ((lane & 31) >> 1) & 7;
-    int soff[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) soff[s] = (lane & 31) * (kBK * 2) + ((((2 * s + hsel) ^ rowx)) << 4);
-
-    // One 64-deep k-step on stage `sb` while stage `nb_` fills with k-step kt+1.
-    // One 64-deep k-step on stage `sb` while stage `nb_` fills with k-step kt+1.
-    // VAR 0: fragment reads / dequant+MFMA in sched_barrier-fenced blocks (reads one substep ahead);
-    // VAR 1: same data flow, compiler-scheduled; VAR 2: A and B fragments both one substep ahead,
-    // MFMAs interleaved with the next substep's ds_reads and dequant VALU by sched_group_barrier;
-    // VAR 3: VAR 2 + s_setprio(1) around each MFMA group.
-    auto read_b = [&](half8_t (&b)[MR], const uint8_t *sb, int s) {
-#pragma unroll
-        for (int r = 0; r < MR; ++r) b[r] = *reinterpret_cast<const half8_t *>(sb + soff[s] + r * 32 * kBK * 2);
-    };
-    auto mfma8 = [&](const half8_t &a, const half8_t (&b)[MR]) {
-#pragma unroll
-        for (int r = 0; r < MR; ++r) acc[r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b[r], acc[r], 0, 0, 0);
-    };
-    auto step = [&](const uint8_t *sb, uint8_t *nb_, unsigned kt) {
-        if (kt + 1 < nk) stage(nb_, kt + 1);
-        uint32_t w[BITS];
-        lds_words<BITS>(w, sb + SL::kX + wave * (64 * BITS * 4), lane);
-        half2_t nz, sc;
-        split_sz(*reinterpret_cast<const uint32_t *>(sb + SL::kX + SL::kW + wave * 256 + lane * 4), nz, sc);
-        half8_t bA[MR], bB[MR];
-        read_b(bA, sb, 0);
-        if constexpr (VAR <= 1) {
-#pragma unroll
-            for (int s = 0; s < 4; s += 2) {
-                read_b(bB, sb, s + 1);
-                if constexpr (VAR == 0) __builtin_amdgcn_sched_barrier(0);
-                mfma8(dequant_frag<BITS>(w, s, nz, sc), bA);
-                if constexpr (VAR == 0) __builtin_amdgcn_sched_barrier(0);
-                if (s + 2 < 4) read_b(bA, sb, s + 2);
-                if constexpr (VAR == 0) __builtin_amdgcn_sched_barrier(0);
-                mfma8(dequant_frag<BITS>(w, s + 1, nz, sc), bB);
-                if constexpr (VAR == 0) __builtin_amdgcn_sched_barrier(0);
-            }
-        } else {
-            half8_t aA = dequant_frag<BITS>(w, 0, nz, sc), aB;
-            auto sub = [&](half8_t (&bc)[MR], half8_t (&bn)[MR], const half8_t &ac, half8_t &an, int s) {
-                __builtin_amdgcn_sched_barrier(0);
-                if constexpr (VAR == 3) __builtin_amdgcn_s_setprio(1);
-                if (s < 3) {
-                    read_b(bn, sb, s + 1);
-                    an = dequant_frag<BITS>(w, s + 1, nz, sc);
-                }
-                mfma8(ac, bc);
-#pragma unroll
-                for (int i = 0; i < MR; ++i) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
-                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
-                    __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);   // VALU
-                }
-                if constexpr (VAR == 3) __builtin_amdgcn_s_setprio(0);
-                __builtin_amdgcn_sched_barrier(0);
-            };
-            sub(bA, bB, aA, aB, 0);
-            sub(bB, bA, aB, aA, 1);
-            sub(bA, bB, aA, aB, 2);
-            sub(bB, bA, aB, aA, 3);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    };
-
-    stage(smem0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (unsigned kt = 0; kt < nk; kt += 2) {
-        step(smem0, smem1, kt);
-        if (kt + 1 < nk) step(smem1, smem0, kt + 1);
-    }
-
-    // Epilogue: acc[r] reg e -> n = n0 + 32*wave + (e&3) + 8*(e>>2) + 4*hsel, m = m0 + 32r + (lane&31).
-    const int nb0 = n0 + wave * 32 + 4 * hsel;
-    if constexpr (SPLIT) {
-        // Partial tile (rows < M, all Npad columns exist in the slab): 16-B stores, no bias.
-        float *slab = ws + static_cast<size_t>(ks) * M * Npad;
-#pragma unroll
-        for (int r = 0; r < MR; ++r) {
-            const int m = m0 + r * 32 + (lane & 31);
-            if (m >= M) continue;
-            float *prow = slab + static_cast<size_t>(m) * Npad + nb0;
-#pragma unroll
-            for (int qd = 0; qd < 4; ++qd)
-                *reinterpret_cast<float4 *>(prow + 8 * qd) =
-                    make_float4(acc[r][4 * qd + 0], acc[r][4 * qd + 1], acc[r][4 * qd + 2], acc[r][4 * qd + 3]);
-        }
-        return;
-    }
-    float4 bv[4];
-#pragma unroll
-    for (int qd = 0; qd < 4; ++qd) bv[qd] = *reinterpret_cast<const float4 *>(bias + nb0 + 8 * qd);
-    const bool full = (m0 + kBMt <= M) && (n0 + kBN <= N) && (N % 4) == 0;
-    if (full) {
-#pragma unroll
-        for (int r = 0; r < MR; ++r) {
-            YT *yrow = Y + static_cast<size_t>(m0 + r * 32 + (lane & 31)) * N + nb0;
-#pragma unroll
-            for (int qd = 0; qd < 4; ++qd)
-                store4<YT>(yrow + 8 * qd, acc[r][4 * qd + 0] + bv[qd].x, acc[r][4 * qd + 1] + bv[qd].y,
-                           acc[r][4 * qd + 2] + bv[qd].z, acc[r][4 * qd + 3] + bv[qd].w);
-        }
-    } else {
-        const bool vec_ok = (N % 4) == 0;
-#pragma unroll
-        for (int r = 0; r < MR; ++r) {
-            const int m = m0 + r * 32 + (lane & 31);
-            if (m >= M) continue;
-            YT *yrow = Y + static_cast<size_t>(m) * N;
-#pragma unroll
-            for (int qd = 0; qd < 4; ++qd)
-                store_out4<YT>(yrow, bias, nb0 + 8 * qd, N, vec_ok, acc[r][4 * qd + 0], acc[r][4 * qd + 1],
-                               acc[r][4 * qd + 2], acc[r][4 * qd + 3]);
-        }
-    }
-}
-
-#endif  // DLLM_LAB
+#if DLLM_LAB   // the round-1 prefill GEMM schedules (lab variants 0-3)
+#include "lab/wq_gemm_round1.inc"
+#endif
 
 // ---------------------------------------------------------------------------------------------
 // Big-tile prefill GEMM (used when it still fills the chip): block tile 256 (m) x 256 (n), 8 waves
@@ -1057,389 +804,9 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
     }
 }
 
-#if DLLM_LAB   // lab build only
-// 256 x 256 ring GEMM with the 2 (m) x 4 (n) wave layout: wave (rm, cg) = (wave / 4, wave % 4) owns
-// rows m0 + 128 rm .. +128 (4 m-reps) and columns n0 + 64 cg .. +64 (two 32-column fragments), so
-// each B fragment read from LDS feeds two MFMAs (half the LDS read traffic of the 1 x 8 layout of
-// wq_gemm8_kernel<8, 8>, which measured its DMA ring serialised behind the fragment reads) for
-// twice the dequant VALU per MFMA.  Stage layout and LDS-DMA pattern are those of
-// wq_gemm8_kernel<NW = 8, MR = 8>: wave w stages X rounds, weight fragment w and its scales.
-template <int BITS, typename YT, bool SPLIT = false, int EPI = 0>
-__global__ void __launch_bounds__(512, 1)
-wq_gemm_w2_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdev,
-                  const uint32_t *__restrict__ sz, const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad,
-                  int group, int nbm, int nbn, int nsplit = 1, float *__restrict__ ws = nullptr,
-                  PSampleEpi epi = PSampleEpi{}) {
-    using SL = StageLayout8<BITS, 8, 8, 1>;
-    constexpr int kRep = 4, kFr = 2;
-    __shared__ __attribute__((aligned(16))) uint8_t st0[SL::kBytes];
-    __shared__ __attribute__((aligned(16))) uint8_t st1[SL::kBytes];
-    __shared__ __attribute__((aligned(16))) uint8_t st2[SL::kBytes];
-
-    const int nb = nbm * nbn * nsplit, orig = blockIdx.x;
-    const int xcd = orig % kXCDs, q8 = nb / kXCDs, r8 = nb % kXCDs;
-    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / kXCDs;
-    const int ks = wgid / (nbm * nbn), tile = wgid % (nbm * nbn);
-    const int bm = tile / nbn, bn = tile % nbn;
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int rm = wave >> 2, cg = wave & 3;
-    const int m0 = bm * 256, n0 = bn * 256;
-    const unsigned nk_all = static_cast<unsigned>(K) / kBK;
-    const unsigned nk = nk_all / static_cast<unsigned>(nsplit);
-    const unsigned kt0 = static_cast<unsigned>(ks) * nk;
-    const unsigned kpg = static_cast<unsigned>(group) / kBK;
-
-    // Staging (as wq_gemm8_kernel<8, 8>): wave w loads X rounds, weight fragment w, scales of w.
-    const int chunk_st = lane & 7;
-    const __half *xsrc[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int row = (i * 8 + wave) * 8 + (lane >> 3);
-        int grow = m0 + row;
-        grow = grow < M ? grow : M - 1;
-        const int c = chunk_st ^ ((row >> 1) & 7);
-        xsrc[i] = X + static_cast<size_t>(grow) * K + c * 8;
-    }
-    const unsigned ntw = static_cast<unsigned>(n0 + wave * 32) >> 5;
-    const uint32_t *wsrc = wdev + (static_cast<size_t>(ntw) * nk_all * 64 + lane) * BITS;
-    const uint32_t *szsrc = sz + n0 + wave * 32 + (lane & 31);
-    const uint32_t wv = static_cast<uint32_t>(wave);
-    auto stage = [&](uint8_t *sb, unsigned kt) {
-        const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(sb));
-        kt += kt0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) glds16_asm(xsrc[i] + kt * kBK, base + wv * 1024 + i * 8192);
-        const uint32_t *wp = wsrc + static_cast<size_t>(kt) * 64 * BITS;
-        const uint32_t wb = base + SL::kX + wv * (64 * BITS * 4);
-        if constexpr (BITS == 4) {
-            glds16_asm(wp, wb);
-        } else if constexpr (BITS == 8) {
-            glds16_asm(wp, wb);
-            glds16_asm(wp + 4, wb + 64 * 16);
-        } else {
-            glds4_asm(wp, wb);
-            glds4_asm(wp + 1, wb + 256);
-        }
-        glds4_asm(szsrc + (kt / kpg) * Npad, base + SL::kX + SL::kW + wv * 256);
-    };
-
-    float16_t acc[kFr][kRep];
-#pragma unroll
-    for (int f = 0; f < kFr; ++f)
-#pragma unroll
-        for (int r = 0; r < kRep; ++r)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[f][r][e] = 0.0f;
-
-    const int hsel = lane >> 5;
-    const int rowx = ((lane & 31) >> 1) & 7;
-    int soff[4];
-#pragma unroll
-    for (int s2 = 0; s2 < 4; ++s2) soff[s2] = (rm * 128 + (lane & 31)) * (kBK * 2) + ((((2 * s2 + hsel) ^ rowx)) << 4);
-
-    auto read_b = [&](half8_t (&b)[kRep], const uint8_t *sb, int s2) {
-#pragma unroll
-        for (int r = 0; r < kRep; ++r) b[r] = *reinterpret_cast<const half8_t *>(sb + soff[s2] + r * 32 * kBK * 2);
-    };
-    auto step = [&](const uint8_t *sb, uint8_t *pf, unsigned kt) {
-        const bool issue = kt + 2 < nk;
-        if (issue) stage(pf, kt + 2);
-        uint32_t w[kFr][BITS];
-        half2_t nz[kFr], sc[kFr];
-#pragma unroll
-        for (int f = 0; f < kFr; ++f) {
-            const int fr = 2 * cg + f;
-            lds_words<BITS>(w[f], sb + SL::kX + fr * (64 * BITS * 4), lane);
-            split_sz(*reinterpret_cast<const uint32_t *>(sb + SL::kX + SL::kW + fr * 256 + lane * 4), nz[f], sc[f]);
-        }
-        half8_t bA[kRep], bB[kRep];
-        half8_t aA[kFr], aB[kFr];
-        read_b(bA, sb, 0);
-#pragma unroll
-        for (int f = 0; f < kFr; ++f) aA[f] = dequant_frag<BITS>(w[f], 0, nz[f], sc[f]);
-        auto sub = [&](half8_t (&bc)[kRep], half8_t (&bn)[kRep], const half8_t (&ac)[kFr], half8_t (&an)[kFr], int s2) {
-            __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_setprio(1);
-            if (s2 < 3) {
-                read_b(bn, sb, s2 + 1);
-#pragma unroll
-                for (int f = 0; f < kFr; ++f) an[f] = dequant_frag<BITS>(w[f], s2 + 1, nz[f], sc[f]);
-            }
-#pragma unroll
-            for (int f = 0; f < kFr; ++f)
-#pragma unroll
-                for (int r = 0; r < kRep; ++r)
-                    acc[f][r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac[f], bc[r], acc[f][r], 0, 0, 0);
-#pragma unroll
-            for (int i = 0; i < kFr * kRep; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                if (i < kRep) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-            }
-            __builtin_amdgcn_s_setprio(0);
-            __builtin_amdgcn_sched_barrier(0);
-        };
-        sub(bA, bB, aA, aB, 0);
-        sub(bB, bA, aB, aA, 1);
-        sub(bA, bB, aA, aB, 2);
-        sub(bB, bA, aB, aA, 3);
-        if (issue) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kOps0) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-    };
-
-    stage(st0, 0);
-    if (nk > 1) stage(st1, 1);
-    if (nk > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SL::kOps0) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    for (unsigned kt = 0; kt < nk; kt += 3) {
-        step(st0, st2, kt);
-        if (kt + 1 < nk) step(st1, st0, kt + 1);
-        if (kt + 2 < nk) step(st2, st1, kt + 2);
-    }
-
-    // Epilogue: acc[f][r] reg e -> n = n0 + 32 (2 cg + f) + (e&3) + 8 (e>>2) + 4 hsel,
-    //                              m = m0 + 128 rm + 32 r + (lane&31).
-#pragma unroll
-    for (int f = 0; f < kFr; ++f) {
-        const int nb0 = n0 + (2 * cg + f) * 32 + 4 * hsel;
-        if constexpr (SPLIT) {
-            float *slab = ws + static_cast<size_t>(ks) * M * Npad;
-#pragma unroll
-            for (int r = 0; r < kRep; ++r) {
-                const int m = m0 + rm * 128 + r * 32 + (lane & 31);
-                if (m >= M) continue;
-                float *prow = slab + static_cast<size_t>(m) * Npad + nb0;
-#pragma unroll
-                for (int qd = 0; qd < 4; ++qd)
-                    *reinterpret_cast<float4 *>(prow + 8 * qd) = make_float4(
-                        acc[f][r][4 * qd + 0], acc[f][r][4 * qd + 1], acc[f][r][4 * qd + 2], acc[f][r][4 * qd + 3]);
-            }
-            continue;
-        }
-        float4 bv[4];
-#pragma unroll
-        for (int qd = 0; qd < 4; ++qd) bv[qd] = *reinterpret_cast<const float4 *>(bias + nb0 + 8 * qd);
-        if constexpr (EPI == 1) {
-#pragma unroll
-            for (int r = 0; r < kRep; ++r) {
-                const int m = m0 + rm * 128 + r * 32 + (lane & 31);
-                if (m >= M) continue;
-#pragma unroll
-                for (int qd = 0; qd < 4; ++qd) {
-                    if (nb0 + 8 * qd >= N) continue;
-                    psample4(epi, m, nb0 + 8 * qd, N, acc[f][r][4 * qd + 0] + bv[qd].x, acc[f][r][4 * qd + 1] + bv[qd].y,
-                             acc[f][r][4 * qd + 2] + bv[qd].z, acc[f][r][4 * qd + 3] + bv[qd].w);
-                }
-            }
-            continue;
-        }
-        const bool full = (m0 + 256 <= M) && (n0 + 256 <= N) && (N % 4) == 0;
-        if (full) {
-#pragma unroll
-            for (int r = 0; r < kRep; ++r) {
-                YT *yrow = Y + static_cast<size_t>(m0 + rm * 128 + r * 32 + (lane & 31)) * N + nb0;
-#pragma unroll
-                for (int qd = 0; qd < 4; ++qd)
-                    store4<YT>(yrow + 8 * qd, acc[f][r][4 * qd + 0] + bv[qd].x, acc[f][r][4 * qd + 1] + bv[qd].y,
-                               acc[f][r][4 * qd + 2] + bv[qd].z, acc[f][r][4 * qd + 3] + bv[qd].w);
-            }
-        } else {
-            const bool vec_ok = (N % 4) == 0;
-#pragma unroll
-            for (int r = 0; r < kRep; ++r) {
-                const int m = m0 + rm * 128 + r * 32 + (lane & 31);
-                if (m >= M) continue;
-                YT *yrow = Y + static_cast<size_t>(m) * N;
-#pragma unroll
-                for (int qd = 0; qd < 4; ++qd)
-                    store_out4<YT>(yrow, bias, nb0 + 8 * qd, N, vec_ok, acc[f][r][4 * qd + 0], acc[f][r][4 * qd + 1],
-                                   acc[f][r][4 * qd + 2], acc[f][r][4 * qd + 3]);
-            }
-        }
-    }
-}
-
-// 256 x 256 ring GEMM on the 16x16x32 MFMA (same tile, waves, LDS-DMA ring and staging as
-// wq_gemm8_kernel<8, 8>, weights in the w16 layout): wave w owns columns n0 + 32 w .. +32 as two
-// 16-column fragments f and all 256 rows as 16 m-reps of 16; a 64-deep k-step is 2 substeps of
-// 32, each 4 quarters of 8 MFMAs (2 f x 4 reps) with the next quarter's X fragments prefetched.
-// Accumulator acc[f][r] reg i: token m = m0 + 16 r + (lane & 15), column
-// n = n0 + 32 w + 16 f + 4 (lane >> 4) + i.  (On random data the 16x16x32 shape holds a higher
-// clock under DVFS than the 32x32x16 one at equal cycles per FLOP: MI355X_MICROARCH.md item 7.)
-typedef float float4_t16 __attribute__((ext_vector_type(4)));
-template <int BITS, typename YT, int EPI = 0>
-__global__ void __launch_bounds__(512, 1)
-wq_gemm16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ w16,
-                 const uint32_t *__restrict__ sz, const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad,
-                 int group, int nbm, int nbn, PSampleEpi epi = PSampleEpi{}) {
-    using SL = StageLayout8<BITS, 8, 8, 1>;
-    constexpr int kRep = 16;
-    __shared__ __attribute__((aligned(16))) uint8_t st0[SL::kBytes];
-    __shared__ __attribute__((aligned(16))) uint8_t st1[SL::kBytes];
-    __shared__ __attribute__((aligned(16))) uint8_t st2[SL::kBytes];
-
-    const int nb = nbm * nbn, orig = blockIdx.x;
-    const int xcd = orig % kXCDs, q8 = nb / kXCDs, r8 = nb % kXCDs;
-    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / kXCDs;
-    const int bm = wgid / nbn, bn = wgid % nbn;
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int m0 = bm * 256, n0 = bn * 256;
-    const unsigned nk = static_cast<unsigned>(K) / kBK;
-    const unsigned kpg = static_cast<unsigned>(group) / kBK;
-
-    const int chunk_st = lane & 7;
-    const __half *xsrc[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int row = (i * 8 + wave) * 8 + (lane >> 3);
-        int grow = m0 + row;
-        grow = grow < M ? grow : M - 1;
-        const int c = chunk_st ^ ((row >> 1) & 7);
-        xsrc[i] = X + static_cast<size_t>(grow) * K + c * 8;
-    }
-    const unsigned nt = static_cast<unsigned>(n0 + wave * 32) >> 5;
-    const uint32_t *wsrc = w16 + (static_cast<size_t>(nt) * nk * 64 + lane) * BITS;
-    const uint32_t *szsrc = sz + n0 + 4 * lane;   // 256 columns = 64 lanes x 16 B
-    const uint32_t wv = static_cast<uint32_t>(wave);
-    auto stage = [&](uint8_t *sb, unsigned kt) {
-        const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(sb));
-#pragma unroll
-        for (int i = 0; i < 4; ++i) glds16_asm(xsrc[i] + kt * kBK, base + wv * 1024 + i * 8192);
-        const uint32_t *wp = wsrc + static_cast<size_t>(kt) * 64 * BITS;
-        const uint32_t wb = base + SL::kX + wv * (64 * BITS * 4);
-        if constexpr (BITS == 4) {
-            glds16_asm(wp, wb);
-        } else if constexpr (BITS == 8) {
-            glds16_asm(wp, wb);
-            glds16_asm(wp + 4, wb + 64 * 16);
-        } else {
-            glds4_asm(wp, wb);
-            glds4_asm(wp + 1, wb + 256);
-        }
-        if (wave == 0) glds16_asm(szsrc + (kt / kpg) * Npad, base + SL::kX + SL::kW);
-    };
-    auto wait_prev = [&]() {
-        if (wave == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 + SL::kWOps + 1) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 + SL::kWOps) : "memory");
-    };
-
-    float4_t16 acc[2][kRep];
-#pragma unroll
-    for (int f = 0; f < 2; ++f)
-#pragma unroll
-        for (int r = 0; r < kRep; ++r) acc[f][r] = float4_t16{0.f, 0.f, 0.f, 0.f};
-
-    // X fragment (B operand): lane reads row 16 r + (lane & 15), k chunk 4 s + (lane >> 4), swizzled
-    // by the row's (row >> 1) & 7 (the same for every r: conflict-free in each 16-lane group).
-    const int rl = lane & 15;
-    int soff[2];
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) soff[s2] = rl * (kBK * 2) + (((4 * s2 + (lane >> 4)) ^ ((rl >> 1) & 7)) << 4);
-    auto read_b4 = [&](half8_t (&b)[4], const uint8_t *sb, int s2, int q) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            b[i] = *reinterpret_cast<const half8_t *>(sb + soff[s2] + (4 * q + i) * 16 * kBK * 2);
-    };
-
-    auto step = [&](const uint8_t *sb, uint8_t *pf, unsigned kt) {
-        const bool issue = kt + 2 < nk;
-        if (issue) stage(pf, kt + 2);
-        uint32_t w[BITS];
-        lds_words<BITS>(w, sb + SL::kX + wave * (64 * BITS * 4), lane);
-        half2_t nz[2], sc[2];
-#pragma unroll
-        for (int f = 0; f < 2; ++f)
-            split_sz(*reinterpret_cast<const uint32_t *>(sb + SL::kX + SL::kW + (wave * 32 + 16 * f + rl) * 4), nz[f],
-                     sc[f]);
-        half8_t a0[2], a1[2];
-#pragma unroll
-        for (int f = 0; f < 2; ++f) a0[f] = dequant_frag<BITS>(w, 2 * f + 0, nz[f], sc[f]);
-        half8_t bA[4], bB[4];
-        read_b4(bA, sb, 0, 0);
-        auto sub = [&](half8_t (&bc)[4], half8_t (&bn)[4], const half8_t (&ac)[2], int i) {
-            __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_setprio(1);
-            if (i < 7) read_b4(bn, sb, (i + 1) >> 2, (i + 1) & 3);
-            if (i == 3) {
-#pragma unroll
-                for (int f = 0; f < 2; ++f) a1[f] = dequant_frag<BITS>(w, 2 * f + 1, nz[f], sc[f]);
-            }
-#pragma unroll
-            for (int f = 0; f < 2; ++f)
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    acc[f][4 * (i & 3) + r] =
-                        __builtin_amdgcn_mfma_f32_16x16x32_f16(ac[f], bc[r], acc[f][4 * (i & 3) + r], 0, 0, 0);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                if (j < 4) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-            }
-            __builtin_amdgcn_s_setprio(0);
-            __builtin_amdgcn_sched_barrier(0);
-        };
-        sub(bA, bB, a0, 0);
-        sub(bB, bA, a0, 1);
-        sub(bA, bB, a0, 2);
-        sub(bB, bA, a0, 3);
-        sub(bA, bB, a1, 4);
-        sub(bB, bA, a1, 5);
-        sub(bA, bB, a1, 6);
-        sub(bB, bA, a1, 7);
-        if (issue) wait_prev();
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-    };
-
-    stage(st0, 0);
-    if (nk > 1) stage(st1, 1);
-    if (nk > 1) wait_prev();
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    for (unsigned kt = 0; kt < nk; kt += 3) {
-        step(st0, st2, kt);
-        if (kt + 1 < nk) step(st1, st0, kt + 1);
-        if (kt + 2 < nk) step(st2, st1, kt + 2);
-    }
-
-    const bool vec_ok = (N % 4) == 0;
-#pragma unroll
-    for (int f = 0; f < 2; ++f) {
-        const int nb0 = n0 + wave * 32 + 16 * f + 4 * (lane >> 4);
-        const float4 bv = *reinterpret_cast<const float4 *>(bias + nb0);
-        const bool full = (m0 + 256 <= M) && (nb0 + 4 <= N) && vec_ok;
-#pragma unroll
-        for (int r = 0; r < kRep; ++r) {
-            const int m = m0 + 16 * r + rl;
-            if constexpr (EPI == 1) {
-                if (m < M && nb0 < N)
-                    psample4(epi, m, nb0, N, acc[f][r][0] + bv.x, acc[f][r][1] + bv.y, acc[f][r][2] + bv.z,
-                             acc[f][r][3] + bv.w);
-            } else if (full) {
-                store4<YT>(Y + static_cast<size_t>(m) * N + nb0, acc[f][r][0] + bv.x, acc[f][r][1] + bv.y,
-                           acc[f][r][2] + bv.z, acc[f][r][3] + bv.w);
-            } else if (m < M) {
-                store_out4<YT>(Y + static_cast<size_t>(m) * N, bias, nb0, N, vec_ok, acc[f][r][0], acc[f][r][1],
-                               acc[f][r][2], acc[f][r][3]);
-            }
-        }
-    }
-}
-
-#endif  // DLLM_LAB
+#if DLLM_LAB   // the 256 x 256 ring / ping-pong GEMM schedules (lab variants 4-15)
+#include "lab/wq_ring256.inc"
+#endif
 
 // ---------------------------------------------------------------------------------------------
 // Decode GEMM (small M, weight-streaming / HBM-bound): one block per 16 NT-column group and
@@ -1808,94 +1175,9 @@ int launch_ring(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t
     return DLLM_OK;
 }
 
-#if DLLM_LAB
-// Lab schedules (variants 0..3 and 5..13; see dllm_linear_set_kernel_variant).  Returns -1 when
-// the variant does not apply to this shape (the product policy runs instead).
-template <int BITS, typename YT, int VAR>
-void launch_prefill(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t st) {
-    const int nbm = (M + kBM - 1) / kBM, nbn = static_cast<int>(h->Npad / kBN);
-    const unsigned nb = static_cast<unsigned>(nbm) * nbn;
-    wq_gemm_kernel<BITS, YT, VAR><<<nb, kThreads, 0, st>>>(X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N,
-                                                           (int)h->Npad, (int)h->group, nbm, nbn);
-}
-
-template <int BITS, typename YT>
-int launch_mid(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t st) {
-    constexpr int MR = 4;
-    const int nbm = (M + 32 * MR - 1) / (32 * MR), nbn = static_cast<int>(h->Npad / kBN);
-    const int tiles = nbm * nbn;
-    const int nk = static_cast<int>(h->K / kBK);
-    int nsplit = 1;
-    while (tiles * nsplit < 200 && nsplit < 8 && nk % (2 * nsplit) == 0 && nk / (2 * nsplit) >= 4) nsplit *= 2;
-    const unsigned nb = static_cast<unsigned>(tiles * nsplit);
-    if (nsplit == 1) {
-        wq_gemm_kernel<BITS, YT, 3, MR, false><<<nb, kThreads, 0, st>>>(
-            X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn);
-        DLLM_LAUNCH_CHECK();
-        return DLLM_OK;
-    }
-    float *ws = device_workspace(st, static_cast<size_t>(nsplit) * M * h->Npad * sizeof(float));
-    if (!ws) return DLLM_ERR_HIP;
-    wq_gemm_kernel<BITS, YT, 3, MR, true><<<nb, kThreads, 0, st>>>(
-        X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn, nsplit, ws);
-    DLLM_LAUNCH_CHECK();
-    const size_t q = static_cast<size_t>(M) * (h->Npad / 4);
-    const unsigned rb = static_cast<unsigned>(std::min<size_t>((q + 255) / 256, 4 * kCUs));
-    splitk_reduce_kernel<YT><<<rb, 256, 0, st>>>(ws, nsplit, M, (int)h->N, (int)h->Npad, h->bias, Y);
-    DLLM_LAUNCH_CHECK();
-    return DLLM_OK;
-}
-
-template <int BITS, typename YT, int EPI>
-int launch_lab_variant(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t st, const PSampleEpi *epi) {
-    const int np = static_cast<int>(h->Npad);
-    const int mb256 = (M + 255) / 256, mb128 = (M + 127) / 128;
-    const PSampleEpi ep = epi ? *epi : PSampleEpi{};
-    const int v = h->variant;
-    if (EPI == 0 && v >= 0 && v <= 3) {
-        switch (v) {
-        case 0: launch_prefill<BITS, YT, 0>(h, X, M, Y, st); break;
-        case 1: launch_prefill<BITS, YT, 1>(h, X, M, Y, st); break;
-        case 2: launch_prefill<BITS, YT, 2>(h, X, M, Y, st); break;
-        default: launch_prefill<BITS, YT, 3>(h, X, M, Y, st); break;
-        }
-        DLLM_LAUNCH_CHECK();
-        return DLLM_OK;
-    }
-    if (EPI == 0 && v == 6) {
-        const int tiles256 = mb256 * static_cast<int>(h->Npad / kBN);
-        if (tiles256 < kCUs) return launch_mid<BITS, YT>(h, X, M, Y, st);
-        launch_prefill<BITS, YT, 3>(h, X, M, Y, st);
-        DLLM_LAUNCH_CHECK();
-        return DLLM_OK;
-    }
-    if (v == 12 && np % 256 == 0 && mb128 * (np / 256) >= kCUs) return launch_ring<BITS, YT, 8, 4, 1, EPI>(h, X, M, Y, st, 1, epi);
-    if (np % 256 == 0 && mb256 * (np / 256) >= kCUs) {
-        if (v >= 9 && v <= 11)   // ping-pong schedules (linear_pp.hip)
-            return launch_pp_gemm(BITS, std::is_same<YT, float>::value ? 1 : 0, X, M, (int)h->K,
-                                  v == 11 ? h->w16 : h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad,
-                                  (int)h->group, v - 8, EPI ? epi : nullptr, st, h->pplab);
-        if (v == 8) {
-            wq_gemm16_kernel<BITS, YT, EPI><<<static_cast<unsigned>(mb256 * (np / 256)), 512, 0, st>>>(
-                X, M, (int)h->K, h->w16, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, mb256, np / 256, ep);
-            DLLM_LAUNCH_CHECK();
-            return DLLM_OK;
-        }
-        if (v == 7) {
-            wq_gemm_w2_kernel<BITS, YT, false, EPI><<<static_cast<unsigned>(mb256 * (np / 256)), 512, 0, st>>>(
-                X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, mb256, np / 256,
-                1, nullptr, ep);
-            DLLM_LAUNCH_CHECK();
-            return DLLM_OK;
-        }
-    }
-    if (v == 13 && np % 256 == 0 && 2 * mb256 * (np / 256) >= kCUs && (h->K / kBK) % 2 == 0)
-        return launch_ring<BITS, YT, 8, 8, 1, EPI>(h, X, M, Y, st, 2, epi);   // 256 x 256, K split 2
-    if (v == 5 && !(np % 256 == 0 && mb256 * (np / 256) >= kCUs) && mb256 * (np / 128) >= kCUs)
-        return launch_ring<BITS, YT, 4, 8, 1, EPI>(h, X, M, Y, st, 1, epi);   // one k-group
-    return -1;
-}
-#endif  // DLLM_LAB
+#if DLLM_LAB   // launchers of the lab schedules
+#include "lab/wq_lab_launch.inc"
+#endif
 
 // Rounded-weight (DLLM_PRECISION_F16W) tile policy: the largest tile that still gives >= 256
 // blocks -- 256 x 256 (8 waves), 256 x 128 (8 waves, two k-groups) -- below that 128 x 128 tiles

@@ -915,35 +915,33 @@ inline int launch_fused(const float *x, size_t n, const float2 *partials, int np
 
 }  // namespace
 
-// quant_resident.hip: quantize_tensor of one or two tensors in one HBM read (returns 1, launching
-// nothing, when they do not fit on chip or the shape is outside its preconditions).
+#if DLLM_LAB
+// lab/quant_resident.hip (lab build only): quantize_tensor of one or two tensors in one HBM read
+// (returns 1, launching nothing, when they do not fit on chip or the shape is outside its
+// preconditions).
 int launch_quantize_resident(const float *const *x, const size_t *n, int nt, const int *bits, uint8_t *const *out,
                              float *const *params, void *ws, size_t ws_bytes, hipStream_t st);
+#endif
 
 namespace {
 
+#if DLLM_LAB
 // The single pass pays one grid-wide hand-off (a few us): below 4 Mi values per tensor the two
 // passes (both in the Infinity Cache) are as fast.
 constexpr size_t kResidentMin = size_t(1) << 22;
-
-// The single-pass resident kernel is an A/B of the lab build (DLLM_QUANT_RESIDENT=1): measured
-// slower than the two passes at every size it holds (8192 x 4096: 60 vs 49 us),
-// so the product runs the two-pass kernels.
-#if DLLM_LAB
-inline bool resident_disabled() {
-    const char *e = std::getenv("DLLM_QUANT_RESIDENT");
-    return !(e && e[0] == '1');
-}
-#else
-inline bool resident_disabled() { return true; }
 #endif
 
-// One or two tensors at one or two widths through the resident kernel; 0 = launched, 1 = not
-// applicable (the caller runs the multi-pass path), else an error code.
+// One or two tensors at one or two widths through the single-pass resident kernel; 0 = launched,
+// 1 = not applicable (the caller runs the multi-pass path), else an error code.  An A/B of the lab
+// build (DLLM_QUANT_RESIDENT=1): measured slower than the two passes at every size it holds
+// (8192 x 4096: 60 vs 49 us), so the product runs the two-pass kernels and
+// does not contain the resident kernel.
 inline int try_resident(int nt, const float *x0, size_t n0, const float *x1, size_t n1, int ba, int bb,
                         uint8_t *o0a, float *p0a, uint8_t *o0b, float *p0b, uint8_t *o1a, float *p1a, uint8_t *o1b,
                         float *p1b, void *ws, size_t wsb, hipStream_t st) {
-    if (resident_disabled() || !fused_width(ba) || (bb && !fused_width(bb))) return 1;
+#if DLLM_LAB
+    const char *e = std::getenv("DLLM_QUANT_RESIDENT");
+    if (!(e && e[0] == '1') || !fused_width(ba) || (bb && !fused_width(bb))) return 1;
     if (n0 < kResidentMin || (nt > 1 && n1 < kResidentMin)) return 1;
     const float *x[2] = {x0, x1};
     const size_t n[2] = {n0, n1};
@@ -951,6 +949,11 @@ inline int try_resident(int nt, const float *x0, size_t n0, const float *x1, siz
     uint8_t *out[4] = {o0a, o0b, o1a, o1b};
     float *params[4] = {p0a, p0b, p1a, p1b};
     return launch_quantize_resident(x, n, nt, bits, out, params, ws, wsb, st);
+#else
+    (void)nt; (void)x0; (void)n0; (void)x1; (void)n1; (void)ba; (void)bb; (void)o0a; (void)p0a; (void)o0b;
+    (void)p0b; (void)o1a; (void)p1a; (void)o1b; (void)p1b; (void)ws; (void)wsb; (void)st;
+    return 1;
+#endif
 }
 
 template <int BA>
