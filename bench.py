@@ -17,7 +17,8 @@ so ``value`` = 4096 tokens per step / max-over-ranks step time ("scaling": "stro
 collective on that data path (a Megatron column layer hands its Y slice to the row-parallel
 layer after it); the all-gather of the full Y, for a caller that needs it, is timed separately
 (``with_allgather``).  Token-parallel replicas (each rank its own 4096 tokens) are a side key
-(``replicas``, weak scaling), and config C5 hidden-dim sharded over RCCL is ``denoise_loop_tp``.
+(``replicas``, weak scaling), config C5 hidden-dim sharded over RCCL is ``denoise_loop_tp`` and C5
+token-parallel (each rank its 2048 / N tokens of the sample, replicated weights) ``denoise_loop_dp``.
 """
 from __future__ import annotations
 
@@ -310,6 +311,51 @@ def denoise_loop_tp(d, torch, dist, dev, world, steps):
     return res
 
 
+def denoise_loop_dp(d, torch, dist, dev, world, steps):
+    """Config C5 token-parallel over the job's ranks (SURVEY.md 8e's exchange-free form): rank r runs
+    its 2048 / N token rows (parallel.token_rows) of the same sample through the same 12 int4 layers
+    (replicated weights: the linear layers and p_sample are per token), drawing the noise those rows
+    get in the unsharded loop (DenoiseLoop noise_rows), with its token rows of K, V [1, 2048, 4096]
+    in the sharded phase-aware cache (parallel.HeadParallelKVCacheEntry: one all_reduce(MAX) of 4
+    floats per quantization, both widths from it).  The same work per step as ``denoise_loop``;
+    timed between barriers, max over ranks.  Serial schedule (the KV step and its 4-float
+    all-reduce in stream order before the layers)."""
+    par = d.parallel
+    dm, M, L = 4096, 2048, 12
+    rank = dist.get_rank()
+    r0, r1 = par.token_rows(M, world, rank)
+    g = torch.Generator(device=dev).manual_seed(99)
+    layers = [d.QuantLinear.from_weight((0.5 / 64.0) * torch.randn(dm, dm, device=dev, generator=g), None, 4, 128,
+                                        prefill_only=True) for _ in range(L)]
+    cfg = d.DiffusionConfig(num_timesteps=steps, hidden_size=dm, num_layers=L)
+    K = torch.randn(1, M, dm, device=dev, generator=g)
+    V = torch.randn(1, M, dm, device=dev, generator=g)
+    x = torch.randn(M, dm, device=dev, generator=g)[r0:r1].contiguous()
+    kv = par.HeadParallelKVCacheEntry(K[:, r0:r1].contiguous(), V[:, r0:r1].contiguous(), cfg.prefill_bits,
+                                      cfg.decode_bits)
+    del K, V
+    loop = d.DenoiseLoop(layers, cfg, cumprod=d.Cumprod.INCLUSIVE, seed=1, kv_cache=kv, overlap=False,
+                         noise_rows=(r0, M))
+    loop.sample(x, 2)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    out = loop.sample(x, steps)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    s = float(t.item())
+    res = {"workload": f"C5 token-parallel: {L} x int4-g128 d{dm} layers replicated, {M // world} of {M} tokens "
+                       f"per rank, {steps} steps, KV step on the rank's token rows (one 4-float all_reduce(MAX) per "
+                       f"quantization), p_sample fused in the last layer",
+           "n_ranks": world, "ms_per_step": round(s / steps * 1e3, 4), "tok_per_s_per_step": round(M / (s / steps), 1),
+           "finite": bool(torch.isfinite(out).all())}
+    for lyr in layers:
+        lyr.close()
+    return res
+
+
 def _timed(fn, steps, stream, torch, dist, world, dev):
     """``steps`` calls of ``fn`` bracketed by barrier + synchronize; returns (max-over-ranks wall
     seconds, this rank's HIP-event ms per call on ``stream``)."""
@@ -543,6 +589,8 @@ def main():
         out["denoise_loop"] = denoise_loop(d, torch, dev)
         if world > 1 and args.tp_steps > 0:
             out["denoise_loop_tp"] = denoise_loop_tp(d, torch, dist, dev, world, args.tp_steps)
+        if world > 1:
+            out["denoise_loop_dp"] = denoise_loop_dp(d, torch, dist, dev, world, 50)
     if args.sweep and rank == 0 and world == 1:
         out["m_sweep"] = m_sweep(lin, K, N, args.bits, args.group, torch, dev, stream)
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -409,6 +409,10 @@ class DenoiseLoop:
     The layers may be tensor-parallel (parallel.TensorParallelPair: one reduction per pair, x
     replicated on every rank) and the cache head-sharded (parallel.HeadParallelKVCacheEntry): every
     rank then runs this same loop on its shards, with the same phase, width and noise sequence.
+    Token-parallel (``noise_rows=(row0, rows_total)``, parallel.token_rows): every rank runs its
+    rows of x through replicated layers -- the linear layers and p_sample are per token, so no
+    collective -- with its rows of K/V in a sharded cache (one 4-float all_reduce(MAX) per
+    quantization) and the noise its rows get in the unsharded loop.
     ``ops`` holds the elementwise steps (p_sample, noise) and ``device`` where x lives: the HIP
     kernels on the GPU (``DeviceLoopOps``); the CPU multi-process tests pass the oracle's
     restatement and device "cpu" (serial schedule only)."""
@@ -418,9 +422,15 @@ class DenoiseLoop:
     def __init__(self, layers: Sequence, config: DiffusionConfig, cumprod: Cumprod = Cumprod.INCLUSIVE,
                  alpha_mode: AlphaMode = AlphaMode.PER_SAMPLE, seed: int = 0,
                  kv_cache: Optional[KVCacheEntry] = None, overlap: bool = True, noise: str = "epilogue",
-                 ops=DeviceLoopOps, device="cuda"):
+                 ops=DeviceLoopOps, device="cuda", noise_rows: Optional[tuple] = None):
         if noise not in ("side", "epilogue"):
             raise ValueError("noise must be 'side' or 'epilogue'")
+        # noise_rows = (row0, rows_total): x holds rows row0.. of a rows_total-token sample (a token
+        # shard); step i then draws stream elements [i rows_total d + row0 d, ...), the same noise
+        # those rows get in the unsharded loop
+        if noise_rows is not None and not (0 <= int(noise_rows[0]) < int(noise_rows[1])):
+            raise ValueError("noise_rows must be (row0, rows_total) with 0 <= row0 < rows_total")
+        self.noise_rows = None if noise_rows is None else (int(noise_rows[0]), int(noise_rows[1]))
         self.ops, self.device = ops, torch.device(device)
         if self.device.type != "cuda":
             overlap = False
@@ -445,6 +455,15 @@ class DenoiseLoop:
             self._coef_cache[t] = (torch.from_numpy(coef).to(self.device), bool(flag.value))
         return self._coef_cache[t]
 
+    def _noise_offset(self, step_index: int, M: int, d: int) -> int:
+        """First noise-stream element of step ``step_index`` for this x (its rows of the sample)."""
+        if self.noise_rows is None:
+            return step_index * M * d
+        row0, total = self.noise_rows
+        if row0 + M > total:
+            raise ValueError(f"x has {M} rows from row {row0}: past the sample's {total}")
+        return step_index * total * d + row0 * d
+
     def step(self, x: torch.Tensor, t: int, step_index: int, out: Optional[torch.Tensor] = None,
              noise: Optional[torch.Tensor] = None, noise_ready: Optional[torch.cuda.Event] = None,
              x16: Optional[torch.Tensor] = None, out16: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -453,7 +472,7 @@ class DenoiseLoop:
         the fused last layer's epilogue (the next step's ``x16``), when the last layer is fused."""
         M, d = x.shape
         coef, flag = self._coef(t)
-        offset = step_index * M * d
+        offset = self._noise_offset(step_index, M, d)
         h = x if x16 is None else x16
         for layer in self.layers[:-1]:
             h = layer(h, out_dtype=torch.float16)
@@ -539,7 +558,7 @@ class DenoiseLoop:
             with torch.cuda.stream(side):
                 if freed[j] is not None:
                     side.wait_event(freed[j])
-                self.ops.randn(nz, self.seed, i * M * d)
+                self.ops.randn(nz, self.seed, self._noise_offset(i, M, d))
                 ready = torch.cuda.Event()
                 ready.record(side)
                 self.kv_step(t, num_steps)

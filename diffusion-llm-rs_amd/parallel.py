@@ -17,7 +17,10 @@ straddle a column boundary and K/G is a whole number of groups for G <= 32.  Mod
   (G-1)/G * (4 + 2) B per element instead of the all-reduce's (G-1)/G * 2 * 4 B, and the sum is
   still f32).  The bias is added once, after the reduction.
 * Megatron pairing (column then row, ``TensorParallelPair``): one reduction per layer pair.
-* token-parallel replicas (``TokenParallelLinear``): the full 8 MiB int4 weight per rank.
+* token-parallel (``TokenParallelLinear``, ``token_rows``): the full 8 MiB int4 weight on every
+  rank, rank r runs its token rows with no collective.  For config C5 (DenoiseLoop with
+  ``noise_rows``) each rank also holds its rows of K/V in a ``HeadParallelKVCacheEntry`` (one
+  4-float all_reduce(MAX) per quantization): the bench's ``denoise_loop_dp``.
 
 ``shard=(world, rank)`` builds the shard rank ``rank`` of a ``world``-way split in a process that
 is not part of such a group and disables the collectives (``partial`` gives the un-reduced
@@ -71,6 +74,16 @@ def row_range(K: int, world: int, rank: int, group: int = 128):
     g0 = rank * per + min(rank, rem)
     g1 = g0 + per + (1 if rank < rem else 0)
     return min(g0 * group, K), min(g1 * group, K)
+
+
+def token_rows(M: int, world: int, rank: int):
+    """Contiguous token-row shard [r0, r1) of an M-token batch or sample (token parallelism: the
+    linear layers and p_sample are per token, so rank r runs rows r0..r1 through replicated layers
+    with no collective; in the denoise loop its K/V rows go to a sharded cache,
+    HeadParallelKVCacheEntry)."""
+    per, rem = divmod(M, world)
+    r0 = rank * per + min(rank, rem)
+    return r0, r0 + per + (1 if rank < rem else 0)
 
 
 def _default_factory(W, bias, bits, group):
@@ -259,9 +272,7 @@ class TokenParallelLinear:
         self.local = local_factory(W, bias, bits, group)
 
     def token_range(self, M: int):
-        per, rem = divmod(M, self.world)
-        m0 = self.rank * per + min(self.rank, rem)
-        return m0, m0 + per + (1 if self.rank < rem else 0)
+        return token_rows(M, self.world, self.rank)
 
     def forward(self, x_local: torch.Tensor, out_dtype=torch.float16) -> torch.Tensor:
         return self.local(x_local, out_dtype=out_dtype)
@@ -391,7 +402,9 @@ class HeadParallelKVCacheEntry(KVCacheEntry):
     decode-width per-tensor quantized copy, phase switch, progressive decode widths, re-quantizing
     ``update``) with K and V sharded by head over the ranks: rank r holds the hidden
     columns of its heads (``head_columns``) of K, V ``[layers, seq, hidden]`` as contiguous local
-    tensors.  The phase logic and the accounting (lib.rs:279-302, per shard) are KVCacheEntry's.
+    tensors -- or its token rows (``token_rows``, the token-parallel denoise loop): the quantization
+    below needs only the shard's elements and the global extremes, so any disjoint split works.  The
+    phase logic and the accounting (lib.rs:279-302, per shard) are KVCacheEntry's.
 
     The reference quantizes K and V per WHOLE tensor (quantization.rs:142-150), so a shard's
     params need the global extremes: each quantization folds the local K and V (NaN-ignoring,

@@ -243,3 +243,74 @@ def test_denoise_loop_config5_sharded(dllm, torch, orc, G):
         lin.close()
     for p in pairs:
         p.close()
+
+
+@pytest.mark.parametrize("G", [2, 4, 8])
+def test_denoise_loop_config5_token_parallel(dllm, torch, orc, G):
+    """Config C5 token-parallel (SURVEY.md 8e's exchange-free form; the bench's ``denoise_loop_dp``):
+    G ranks emulated in one process, rank r running tokens parallel.token_rows(2048, G, r) of x
+    through the SAME 12 int4 layers (replicated weights, QuantLinear) with the noise those rows get
+    in the unsharded loop (DenoiseLoop noise_rows), and its token rows of K/V in the sharded cache
+    (tp_emulation.EmulatedHeadParallelKV split="rows": one max of the shards' extremes per
+    quantization).  Teacher-forced per step against the unsharded step and the f32 chain, as
+    test_denoise_loop_config5_sharded: the rank shards' rows run the GEMM at M = 2048 / G (other tile
+    policies, other f32 summation orders), so (a) vs (b) is rounding-level, (a) vs (c) <= 1e-3; the
+    cache's phase, widths, codes and params bit-identical to the unsharded cache's rows."""
+    import json
+    import os
+    par = dllm.parallel
+    d, M, L, steps, seed, heads = 4096, 2048, 12, 50, 7, 32
+    g = torch.Generator(device="cuda").manual_seed(7)
+    Ws = [(1.0 / 64.0) * torch.randn(d, d, device="cuda", generator=g) for _ in range(L)]
+    cfg = dllm.DiffusionConfig(num_timesteps=steps, hidden_size=d, num_layers=L, num_attention_heads=heads)
+    K = torch.randn(1, M, d, device="cuda", generator=g)
+    V = 0.5 * torch.randn(1, M, d, device="cuda", generator=g)
+    x = torch.randn(M, d, device="cuda", generator=g)
+    lins = [dllm.QuantLinear.from_weight(W, None, 4, 128, prefill_only=True) for W in Ws]
+    Wh = [_dequantized(lin, orc) for lin in lins]
+    rows = [par.token_rows(M, G, r) for r in range(G)]
+    loops = [dllm.DenoiseLoop(lins, cfg, cumprod=dllm.Cumprod.INCLUSIVE, seed=seed, overlap=False,
+                              noise_rows=(r0, M)) for r0, _ in rows]
+    loop_u = dllm.DenoiseLoop(lins, cfg, cumprod=dllm.Cumprod.INCLUSIVE, seed=seed, overlap=False)
+    kv_u = dllm.KVCacheEntry.new(K, V, cfg.prefill_bits, cfg.decode_bits)
+    kv_s = emu.EmulatedHeadParallelKV(K, V, cfg.prefill_bits, cfg.decode_bits, heads, G, split="rows")
+    kv_lu = dllm.DenoiseLoop(lins, cfg, kv_cache=kv_u, overlap=False)
+    kv_ls = dllm.DenoiseLoop(lins, cfg, kv_cache=kv_s, overlap=False)
+    errs, errs_u = [], []
+    for i, t in enumerate(range(steps - 1, -1, -1)):
+        kv_lu.kv_step(t, steps)
+        kv_ls.kv_step(t, steps)
+        assert kv_s.is_prefill_phase == kv_u.is_prefill_phase and kv_s.decode_quant_bits == kv_u.decode_quant_bits
+        for qu, qs in ((kv_u.prefill_quantized, kv_s.prefill_quantized), (kv_u.decode_quantized, kv_s.decode_quantized)):
+            assert (qu is None) == (qs is None), i
+            if qu is None:
+                continue
+            for which in ("keys", "values"):
+                full = _unpacked(dllm, getattr(qu, which))
+                pu = getattr(qu, which).params.view(torch.int32)
+                for (r0, r1), sh in zip(kv_s.cols, qs):
+                    part = getattr(sh, which)
+                    assert torch.equal(_unpacked(dllm, part), full[:, r0:r1]), (i, which, r0)
+                    assert torch.equal(part.params.view(torch.int32), pu), (i, which, r0)
+        xs = torch.cat([lp.step(x[r0:r1].contiguous(), t, i) for lp, (r0, r1) in zip(loops, rows)])
+        xu = loop_u.step(x, t, i)
+        coef, flag = dllm.diffusion.p_sample_coeffs(cfg, [t], 1, dllm.Cumprod.INCLUSIVE)
+        c1_, c2_, sd = (float(v) for v in coef[0])
+        nz = dllm.randn(M * d, seed, i * M * d).reshape(M, d) if flag else 0.0
+        h = x
+        for W in Wh:
+            h = h @ W
+        ref = (c1_ * x + c2_ * h) + sd * nz
+        errs.append(_rel(xs, ref))
+        errs_u.append(_rel(xs, xu))
+        x = xs
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open(f"gpurun_out/c5_token_parallel_G{G}.json", "w") as f:
+        json.dump({"G": G, "rel_err_vs_f32_chain": errs, "rel_diff_vs_unsharded_step": errs_u,
+                   "max": max(errs), "max_vs_unsharded": max(errs_u)}, f)
+    print(f"C5 token-parallel G={G}: max rel err vs f32 chain {max(errs):.3e}, vs unsharded step {max(errs_u):.3e}")
+    assert bool(torch.isfinite(x).all())
+    assert max(errs) <= REL_TOL, max(errs)
+    assert max(errs_u) <= REL_TOL, max(errs_u)
+    for lin in lins:
+        lin.close()

@@ -34,14 +34,26 @@ class EmulatedHeadParallelKV:
     lists of shard tensors; ``get_keys``/``get_values`` concatenate the shards' hand-outs along the
     hidden dimension (the unsharded entry's tensor, for comparison)."""
 
-    def __init__(self, keys, values, prefill_bits, decode_bits, num_heads, world, ops=DeviceKVOps):
+    def __init__(self, keys, values, prefill_bits, decode_bits, num_heads, world, ops=DeviceKVOps, split="heads"):
+        """``split="rows"``: the shards are token rows (``parallel.token_rows`` of the seq axis, the
+        token-parallel loop) instead of head columns; ``cols`` then holds the row ranges."""
+        if split not in ("heads", "rows"):
+            raise ValueError("split must be 'heads' or 'rows'")
+        self.split = split
         hidden = keys.shape[-1]
         self.world, self.num_heads = world, num_heads
-        self.cols = [head_columns(hidden, num_heads, world, r) for r in range(world)]
-        ks = [keys[..., c0:c1].contiguous() for c0, c1 in self.cols]
-        vs = [values[..., c0:c1].contiguous() for c0, c1 in self.cols]
+        if split == "heads":
+            self.cols = [head_columns(hidden, num_heads, world, r) for r in range(world)]
+        else:
+            self.cols = [_par.token_rows(keys.shape[1], world, r) for r in range(world)]
+        ks = [self._part(keys, c) for c in self.cols]
+        vs = [self._part(values, c) for c in self.cols]
         red = torch.stack([_local_extremes_of(k, v, ops) for k, v in zip(ks, vs)]).amax(0)
         self.shards = [HeadParallelKVCacheEntry(k, v, prefill_bits, decode_bits, ops=ops, red=red) for k, v in zip(ks, vs)]
+
+    def _part(self, t, c):
+        c0, c1 = c
+        return (t[..., c0:c1] if self.split == "heads" else t[:, c0:c1]).contiguous()
 
     def _reduce_for(self, keys, values):
         red = torch.stack([s.local_extremes(k, v) for s, k, v in zip(self.shards, keys, values)]).amax(0)
@@ -88,17 +100,17 @@ class EmulatedHeadParallelKV:
         return self.shards[0].get_current_quant_bits()
 
     def get_keys(self):
-        return torch.cat([s.get_keys() for s in self.shards], dim=-1)
+        return torch.cat([s.get_keys() for s in self.shards], dim=-1 if self.split == "heads" else 1)
 
     def get_values(self):
-        return torch.cat([s.get_values() for s in self.shards], dim=-1)
+        return torch.cat([s.get_values() for s in self.shards], dim=-1 if self.split == "heads" else 1)
 
     def update(self, new_keys, new_values):
         """KVCacheEntry::update of every shard; ``new_keys``/``new_values`` are the shard lists (as
         ``keys``/``values`` hand them out) or full tensors, which are split by head here."""
         if isinstance(new_keys, torch.Tensor):
-            new_keys = [new_keys[..., c0:c1].contiguous() for c0, c1 in self.cols]
-            new_values = [new_values[..., c0:c1].contiguous() for c0, c1 in self.cols]
+            new_keys = [self._part(new_keys, c) for c in self.cols]
+            new_values = [self._part(new_values, c) for c in self.cols]
         self._reduce_for(new_keys, new_values)
         for s, k, v in zip(self.shards, new_keys, new_values):
             s.update(k, v)
