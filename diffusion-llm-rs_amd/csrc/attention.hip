@@ -139,7 +139,15 @@ __device__ __forceinline__ half2_t pair_qz(uint32_t lo_word_codes, int shift, ha
     return __builtin_bit_cast(half2_t, t) + nz;   // exact
 }
 
-template <int BITS>
+// Position of key k (0..31) within its 32-key group of the 16x16x32 kernel's V image (lab A/B,
+// lab/attn16.inc): key
+// 16 a + 4 g + i at 8 g + 4 a + i, so that the 8 keys a P V B-fragment lane of group g needs
+// ({4 g .. 4 g + 3, 16 + 4 g .. 16 + 4 g + 3}, the two 16-key score blocks' rows of that lane group)
+// sit in one 16-B run.
+__host__ __device__ constexpr int kv_pos16(int k) { return 8 * ((k >> 2) & 3) + 4 * ((k >> 4) & 1) + (k & 3); }
+
+// VL16: the V image in kv_pos16 order (kv_attention16_kernel); else kv_pos (kv_attention5_kernel).
+template <int BITS, bool VL16 = false>
 __device__ __forceinline__ void store_raw(const Raw<BITS> &r, _Float16 (&bk)[kKB][kKRow], _Float16 (&bvt)[kD][kVRow],
                                           int tid, half2_t kz, half2_t vz) {
     constexpr int CPW = 32 / BITS;   // codes per word
@@ -173,7 +181,7 @@ __device__ __forceinline__ void store_raw(const Raw<BITS> &r, _Float16 (&bk)[kKB
         // transposed, 4 consecutive keys of one dim per 8-B store, at the key position of the V
         // image: keys 4..7 and 8..11 of every 16 swap places (kv_pos), so that the 8 keys a PV
         // fragment lane needs (16 s + 4 hh + {0..3, 8..11}) sit in one 16-B run.
-        const int kp4 = (k4 & ~15) | kv_pos(k4 & 15);
+        const int kp4 = VL16 ? (k4 & ~31) | kv_pos16(k4 & 31) : (k4 & ~15) | kv_pos(k4 & 15);
 #pragma unroll
         for (int dd = 0; dd < 8; ++dd)
             *reinterpret_cast<half4_t *>(&bvt[d0 + dd][kp4]) = half4_t{v[0][dd], v[1][dd], v[2][dd], v[3][dd]};
@@ -183,7 +191,7 @@ __device__ __forceinline__ void store_raw(const Raw<BITS> &r, _Float16 (&bk)[kKB
 // Pre-pass: unpack block kb of head h to its LDS image (through LDS, so the stores to the
 // workspace are coalesced 16-B rows).  Keys past S read as code 0 (buffer range check); the
 // attention kernel masks their scores and their P is 0.
-template <int BITS>
+template <int BITS, bool VL16 = false>
 __global__ void __launch_bounds__(512) kv_stage_kernel(const uint8_t *__restrict__ Kq, const float *__restrict__ kp,
                                                       const uint8_t *__restrict__ Vq, const float *__restrict__ vp,
                                                       int S, int H, int nkb, uint8_t *__restrict__ img) {
@@ -198,7 +206,7 @@ __global__ void __launch_bounds__(512) kv_stage_kernel(const uint8_t *__restrict
     const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(Vq), 0, nbytes, 0x00020000);
     Raw<BITS> raw;
     load_raw<BITS>(raw, krs, vrs, tid, kb * kKB, kb * kKB, H, h);
-    store_raw<BITS>(raw, tk, tv, tid, kz, vz);
+    store_raw<BITS, VL16>(raw, tk, tv, tid, kz, vz);
     __syncthreads();
     uint8_t *dst = img + (static_cast<size_t>(h) * nkb + kb) * kImg;
     const uint4 *sk = reinterpret_cast<const uint4 *>(&tk[0][0]);
@@ -563,6 +571,10 @@ kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__
 }
 
 
+#if DLLM_LAB   // attention on 16x16x32 MFMAs (A/B against v5)
+#include "lab/attn16.inc"
+#endif
+
 #if DLLM_LAB   // attention v6 (one wave per SIMD; A/B against v5)
 #include "lab/attn_v6.inc"
 #endif
@@ -570,6 +582,7 @@ kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__
 }  // namespace dllm
 
 using namespace dllm;
+
 
 extern "C" int dllm_kv_attention(const void *Q, const uint8_t *Kq, const float *k_params, const uint8_t *Vq,
                                  const float *v_params, uint8_t bits, size_t S, size_t H, size_t D, void *O,
@@ -588,6 +601,13 @@ extern "C" int dllm_kv_attention(const void *Q, const uint8_t *Kq, const float *
     uint8_t *img = reinterpret_cast<uint8_t *>(device_workspace(st, static_cast<size_t>(H) * nkb * kImg, 8));
     if (!img) return DLLM_ERR_HIP;
     dim3 sgrid(static_cast<unsigned>(nkb), static_cast<unsigned>(H));
+#if DLLM_LAB
+    const int lab = [] { const char *e = getenv("DLLM_ATTN_LAB"); return e ? atoi(e) : 0; }();
+    if (lab == 16) {   // the 16x16x32 kernel (A/B): its V image in kv_pos16 order
+        if (bits == 4) kv_stage_kernel<4, true><<<sgrid, 512, 0, st>>>(Kq, k_params, Vq, v_params, (int)S, (int)H, nkb, img);
+        else kv_stage_kernel<8, true><<<sgrid, 512, 0, st>>>(Kq, k_params, Vq, v_params, (int)S, (int)H, nkb, img);
+    } else
+#endif
     if (bits == 4)
         kv_stage_kernel<4><<<sgrid, 512, 0, st>>>(Kq, k_params, Vq, v_params, (int)S, (int)H, nkb, img);
     else
@@ -602,8 +622,10 @@ extern "C" int dllm_kv_attention(const void *Q, const uint8_t *Kq, const float *
     // (valid results); 100 + mask: the same masks on the v5 kernel, plus 16 no vmcnt wait at the
     // end of a k-block, 32 no barrier there, 64 register staging instead of LDS-DMA (valid
     // results); 200 (+ mask): v6.  Read per call so that a script can A/B the schedules in one process.
-    const int lab = [] { const char *e = getenv("DLLM_ATTN_LAB"); return e ? atoi(e) : 0; }();
     switch (lab) {
+        case 16:   // the 16x16x32 kernel (A/B)
+            kv_attention16_kernel<<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh);
+            break;
 #define DLLM_ALAB(L) case L: kv_attention_kernel<L><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh); break;
         DLLM_ALAB(1) DLLM_ALAB(2) DLLM_ALAB(3) DLLM_ALAB(4) DLLM_ALAB(5) DLLM_ALAB(6) DLLM_ALAB(7)
         DLLM_ALAB(8) DLLM_ALAB(12) DLLM_ALAB(13) DLLM_ALAB(14) DLLM_ALAB(15)

@@ -39,7 +39,6 @@ namespace {
 constexpr int kHX = 256 * kBK * 2;            // X tile bytes per stage (32 KiB)
 constexpr int kHW = 8 * 1024;                 // 8 waves x 64 lanes x 16 B of weight words
 constexpr int kHG = 2048;                     // sz (1 KiB) + ratios (1 KiB), group-first stages
-constexpr int kHStage = kHX + kHW + kHG;      // 43008 B; 3 stages = 126 KiB
 
 // One wave's stage burst: 4 X pieces (rows (8 i + wave) 8 ..) and its weight words, LDS-DMA
 // through buffer descriptors.  lds0 = this wave's first X destination; the next pieces follow at
