@@ -36,7 +36,6 @@
 namespace dllm {
 namespace {
 
-constexpr int kHX = 256 * kBK * 2;            // X tile bytes per stage (32 KiB)
 constexpr int kHW = 8 * 1024;                 // 8 waves x 64 lanes x 16 B of weight words
 constexpr int kHG = 2048;                     // sz (1 KiB) + ratios (1 KiB), group-first stages
 
