@@ -17,6 +17,7 @@
 //   Per (group, column) one u32 `sz` = f16 pair {-(1024 + zp), f16(scale)}:
 //   f16(q - zp) is exact (|q - zp| < 2048), then one f16 rounding of (q - zp) * f16(scale).
 #include "linear_common.hpp"
+#include "stamp.hpp"
 #include "diffusion_rng.hpp"
 
 #ifndef DLLM_LAB
@@ -822,6 +823,11 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
 // ---------------------------------------------------------------------------------------------
 typedef float float4_t __attribute__((ext_vector_type(4)));
 constexpr int kDecWaves = 8;
+#if DLLM_STAMP
+// phase stamps of wq_decode_kernel (stamp build only): 0 entry, 1 + 2 r / 2 + 2 r round r's loads
+// issued / its MFMAs issued, kEpi the wave partials in LDS, kEnd exit
+DLLM_STAMP_BUFFER(g_stamp_dec);
+#endif
 
 // EXACT (1: group 64, 2: group >= 128): the MFMA A operand is the exact integer (q - zp)
 // (linear_exact.hip) and each slab's partial is folded into the accumulator with the f32 scales of
@@ -848,6 +854,9 @@ wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
     __shared__ __attribute__((aligned(16))) float red[DW * MT * NT * 64 * 4];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    DLLM_STAMP_RT(g_stamp_dec, stamp::kRtEntry);
+    DLLM_STAMP_AT(g_stamp_dec, 0);
+    DLLM_STAMP_IDS(g_stamp_dec);
     const int n0 = blockIdx.x * 16 * NT;
     const int nslab = (K + 127) / 128;
     // this block's K-slice: slabs [s_beg, s_end)
@@ -881,7 +890,8 @@ wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
         for (int mt = 0; mt < MT; ++mt) acc[nt][mt] = float4_t{0.f, 0.f, 0.f, 0.f};
 
     const bool g64 = EXACT == 1;    // two groups per 128-deep slab
-    for (int base = s_beg + wave; base < s_end; base += DW * kDepth) {
+    int round = 0;
+    for (int base = s_beg + wave; base < s_end; base += DW * kDepth, ++round) {
         uint32_t w[kDepth][NT][BITS];
         uint32_t szl[kDepth][NT];
         half8_t xb[kDepth][4][MT];
@@ -928,6 +938,7 @@ wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
         // Keep the scheduler from sinking the loads back next to their MFMAs (it does so to cut
         // register pressure, which turns the round into one serial latency per fragment).
         __builtin_amdgcn_sched_barrier(0);
+        DLLM_STAMP_AT(g_stamp_dec, round < 20 ? 1 + 2 * round : -1);
         if constexpr (EXACT) {
 #pragma unroll
             for (int i = 0; i < kDepth; ++i) {
@@ -977,6 +988,7 @@ wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
                 }
             }
         }
+        DLLM_STAMP_AT(g_stamp_dec, round < 20 ? 2 + 2 * round : -1);
     }
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
@@ -984,6 +996,7 @@ wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
         for (int mt = 0; mt < MT; ++mt)
             *reinterpret_cast<float4_t *>(red + ((wave * MT * NT + nt * MT + mt) * 64 + lane) * 4) = acc[nt][mt];
     __syncthreads();
+    DLLM_STAMP_AT(g_stamp_dec, stamp::kEpi);
     // Wave j sums the 8 partials of tiles j, j + 8, ... (tile = nt * MT + mt) in wave order.
     for (int tile = wave; tile < MT * NT; tile += DW) {
         float4_t s = float4_t{0.f, 0.f, 0.f, 0.f};
@@ -1015,7 +1028,14 @@ wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
             }
         }
     }
+    DLLM_STAMP_AT(g_stamp_dec, stamp::kEnd);
+    DLLM_STAMP_RT(g_stamp_dec, stamp::kRtEnd);
 }
+#if DLLM_STAMP
+}  // namespace
+DLLM_STAMP_READER(dllm_stamp_read_dec, g_stamp_dec)
+namespace {
+#endif
 
 constexpr int kDecodeMaxM = 64;
 
