@@ -53,6 +53,13 @@
 #ifndef DLLM_EXACT_S16
 #define DLLM_EXACT_S16 0
 #endif
+// DLLM_EXACT_STAG = 1: the 128 x 256 int4 g128 tiles run their two wave halves half a step apart
+// (M 2048 / 3072 x 4096: 76.9 -> 73.9 / 121.6 -> 114.0 us, same bits).  The k-group tiles with
+// their k-group halves staggered measured 2-7 % slower (4096 x 1024 / 512, 256 / 512 x 4096) and
+// stay unstaggered (profiles/r05_stag).
+#ifndef DLLM_EXACT_STAG
+#define DLLM_EXACT_STAG 1
+#endif
 #ifndef DLLM_EXACT_KG2
 #define DLLM_EXACT_KG2 1
 #endif
@@ -240,7 +247,8 @@ __device__ __forceinline__ void store_tile_f16_lds_kg(uint8_t *img, const float1
 // of a half come from the same weight words through dequant_exact + v_permlane16_swap (as
 // wq_horner16_kernel), the X tile uses the conflict-free (row >> 1) & 5 chunk swizzle.
 template <int BITS, typename YT, int NW, int MR, int SPS, int KPG, bool SPLIT = false, int EPI = 0, bool TM = false,
-          int TMB = 1, bool WREG = false, int GPS = 1, int RING = 3, int KG = 1, bool HORN = false, bool S16 = false>
+          int TMB = 1, bool WREG = false, int GPS = 1, int RING = 3, int KG = 1, bool HORN = false, bool S16 = false,
+          bool STAG = false>
 __global__ void __launch_bounds__(NW * KG * 64, NW * KG >= 8 ? 1 : 2)
 wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdev,
                      const uint32_t *__restrict__ sz, const float *__restrict__ sf, const float *__restrict__ bias,
@@ -255,6 +263,16 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
     static_assert(RING == 3 || (RING >= 2 && RING <= 8 && !TM), "ring depth");
     static_assert(KG == 1 || (!TM && RING * KG * SL::kBytes >= (KG - 1) * NW * 64 * MR * 16 * 4), "k-group combine fits the ring");
     static_assert(!S16 || (!TM && !HORN), "16x16x32 form: fold kernels");
+    static_assert(!STAG || (!TM && !HORN && !S16 && GPS == 1 && (KG == 1 ? RING >= 4 && NW % 2 == 0 : KG % 2 == 0)),
+                  "staggered halves");
+    // Stage kt + kDist is issued at the head of step kt.  STAG: one half of the block's waves runs
+    // half a step behind the other (one extra barrier at entry; the early half one at exit; a
+    // barrier in the middle of every step), so the halves issue their DMA half a step apart instead
+    // of together.  KG == 1: the halves are waves 0..NW/2-1 / NW/2.. of the one tile; the slot a
+    // step writes was last read by the late half a half step earlier, so the ring keeps one stage
+    // fewer in flight (RING - 2).  KG >= 2: the halves are k-groups 0..KG/2-1 / KG/2.., whose
+    // stage parts are private, so the ring distance is unchanged.
+    constexpr int kDist = (STAG && KG == 1) ? RING - 2 : RING - 1;
     constexpr int kBMt = 32 * MR, kBNt = 32 * NW;
     // RING stages of KG parts each (k-group g's part of stage i at ring + (i KG + g) kBytes)
     __shared__ __attribute__((aligned(16))) uint8_t ring[RING * KG * SL::kBytes];
@@ -354,13 +372,17 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
         if (has_sf) blds16_asm(prs, poff, goff, u(base + SL::kX + SL::kW + SL::kSZ + pg * 1024));
     };
     // Counted wait leaving the newest stage's DMAs (this wave's own count) in flight.
-    // (RING > 3: the RING - 2 newest stages stay in flight.)
-    static_assert((RING - 2) * (SL::kXRounds + SL::kWOps + 1) <= 63, "vmcnt range");
+    // (kDist > 2: the kDist - 1 newest stages stay in flight.)
+    static_assert((kDist - 1) * (SL::kXRounds + SL::kWOps + 1) <= 63, "vmcnt range");
     auto wait_prev = [&]() __attribute__((always_inline)) {
-        if constexpr (RING == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else if (has_sz || has_sf) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((RING - 2) * (SL::kXRounds + SL::kWOps + 1)) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((RING - 2) * (SL::kXRounds + SL::kWOps)) : "memory");
+        if constexpr (kDist == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else if (has_sz || has_sf) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kDist - 1) * (SL::kXRounds + SL::kWOps + 1)) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kDist - 1) * (SL::kXRounds + SL::kWOps)) : "memory");
     };
+    const bool late = STAG && (KG == 1 ? wave >= NW / 2 : kg >= KG / 2);   // STAG: the half running behind
+    // KG == 1: the late half's share of stage kt + 1 is read by the early half from the mid-step
+    // barrier on, so the late half waits for it there; else every wave waits at its own step end.
+    const bool wait_mid = STAG && KG == 1 && late;
 
     float16_t acc[S16 ? 1 : MR], tacc[TM ? TMB : (S16 ? 1 : MR)];
     fx4e_t acc16[S16 ? 2 * MR : 1][2], tacc16[S16 ? 2 * MR : 1][2];
@@ -431,8 +453,8 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
                 for (int j = 0; j < BITS; ++j) w[s][j] = wq[cur][s][j];
             }
         }
-        const bool issue = DLLM_EXACT_ABL != 1 && kt + RING - 1 < nk;
-        if (issue) stage(pf, kt + RING - 1, std::integral_constant<int, (cur + RING - 1) % RING>{});
+        const bool issue = DLLM_EXACT_ABL != 1 && kt + kDist < nk;
+        if (issue) stage(pf, kt + kDist, std::integral_constant<int, (cur + kDist) % RING>{});
         DLLM_STAMP_AT(g_stamp_exact, kt <= stamp::kMaxStep ? 2 + 4 * static_cast<int>(kt) : -1);
         if constexpr (!WREG) {
 #pragma unroll
@@ -632,15 +654,30 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
                               : sub16(bB, bA, std::integral_constant<int, Vs>{})), ...);
             }(std::make_integer_sequence<int, kSub>{});
         } else {
+            // STAG: the mid-step barrier (the other half's step boundary).  The late half's share of
+            // stage kt + 1 must land before it: the early half starts reading kt + 1 right after.
+            auto mid = [&]() __attribute__((always_inline)) {
+                if constexpr (STAG) {
+                    if (wait_mid) {
+                        if (issue) wait_prev();
+                        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    }
+                    __builtin_amdgcn_s_barrier();
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            };
             [&]<int... Vs>(std::integer_sequence<int, Vs...>) __attribute__((always_inline)) {
                 ((Vs % 2 == 0 ? sub(bA, bB, aA, aB, std::integral_constant<int, Vs>{})
-                              : sub(bB, bA, aB, aA, std::integral_constant<int, Vs>{})), ...);
+                              : sub(bB, bA, aB, aA, std::integral_constant<int, Vs>{}),
+                  Vs == kSub / 2 - 1 ? mid() : void()), ...);
             }(std::make_integer_sequence<int, kSub>{});
         }
         // Stage kt+1 must have landed; (RING 3) kt+2's DMAs may stay in flight across the barrier.
         DLLM_STAMP_AT(g_stamp_exact, kt <= stamp::kMaxStep ? 3 + 4 * static_cast<int>(kt) : -1);
-        if (issue) wait_prev();
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (!wait_mid) {
+            if (issue) wait_prev();
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         DLLM_STAMP_AT(g_stamp_exact, kt <= stamp::kMaxStep ? 4 + 4 * static_cast<int>(kt) : -1);
         __builtin_amdgcn_s_barrier();
@@ -712,7 +749,7 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
     // dispatch made hipcc spill ~80 VGPRs).
     auto at = [&](auto i_tag, unsigned kt) __attribute__((always_inline)) {
         constexpr int I = decltype(i_tag)::value;
-        constexpr int cur = I % RING, nxt = (I + RING - 1) % RING;
+        constexpr int cur = I % RING, nxt = (I + kDist) % RING;
         uint8_t *sb = stp(cur) + kpart;
         uint8_t *pf = stp(nxt) + kpart;
         if constexpr (TM) step_tm(sb, pf, kt);
@@ -724,24 +761,26 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
                                       : (KPG == 1 ? RING : (RING % KPG == 0 ? RING : RING * KPG));
 
     stage(stp(0) + kpart, 0, std::integral_constant<int, 0>{});
-    if constexpr (RING >= 3) {
-        // stages 1 .. RING - 2 in flight before the loop (stage kt + RING - 1 is issued in step kt)
+    if constexpr (kDist >= 2) {
+        // stages 1 .. kDist - 1 in flight before the loop (stage kt + kDist is issued in step kt)
         [&]<int... Is>(std::integer_sequence<int, Is...>) __attribute__((always_inline)) {
             ((Is + 1 < static_cast<int>(nk) ? (stage(stp(Is + 1) + kpart, Is + 1, std::integral_constant<int, Is + 1>{}), 0) : 0), ...);
-        }(std::make_integer_sequence<int, RING - 2>{});
-        if (nk >= RING - 1) wait_prev();
+        }(std::make_integer_sequence<int, kDist - 1>{});
+        if (nk >= static_cast<unsigned>(kDist)) wait_prev();
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+    if (late) __builtin_amdgcn_s_barrier();   // STAG: enter half a step behind
     DLLM_STAMP_AT(g_stamp_exact, 1);
     for (unsigned kt = 0; kt < nk; kt += kUnroll) {
         [&]<int... Is>(std::integer_sequence<int, Is...>) __attribute__((always_inline)) {
             ((kt + Is < nk ? (at(std::integral_constant<int, Is>{}, kt + Is), 0) : 0), ...);
         }(std::make_integer_sequence<int, kUnroll>{});
     }
+    if (STAG && !late) __builtin_amdgcn_s_barrier();   // pairs with the late half's last barrier
 
     if constexpr (HORN) {
         // acc = sum_g T_g s_g / s_{G-1}: times the last group's scales
@@ -950,7 +989,7 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
 
 template <int BITS, typename YT, int NW, int MR, int SPS, int KPG, int EPI, bool TM = false, int GPS = 1, int RING = 3,
           int KG = 1, bool WREG = (DLLM_EXACT_WREG != 0 && BITS == 4 && !TM), bool HORN = false,
-          bool S16 = (DLLM_EXACT_S16 != 0 && !TM && !HORN)>
+          bool S16 = (DLLM_EXACT_S16 != 0 && !TM && !HORN), bool STAG = false>
 int launch_exact_tile(const ExactGemmArgs &a, int nsplit, hipStream_t st) {
     if constexpr (HORN) {
         const int nbm = (a.M + 32 * MR - 1) / (32 * MR), nbn = a.Npad / (32 * NW);
@@ -967,14 +1006,14 @@ int launch_exact_tile(const ExactGemmArgs &a, int nsplit, hipStream_t st) {
     const PSampleEpi ep = a.epi ? *a.epi : PSampleEpi{};
     YT *Y = static_cast<YT *>(a.Y);
     if (nsplit == 1) {
-        wq_gemm_exact_kernel<BITS, YT, NW, MR, SPS, KPG, false, EPI, TM, 1, WREG, GPS, RING, KG, false, S16><<<nb, NW * KG * 64, 0, st>>>(
+        wq_gemm_exact_kernel<BITS, YT, NW, MR, SPS, KPG, false, EPI, TM, 1, WREG, GPS, RING, KG, false, S16, STAG><<<nb, NW * KG * 64, 0, st>>>(
             a.X, a.M, a.K, a.wdev, a.sz, a.sf, a.bias, Y, a.N, a.Npad, a.group, nbm, nbn, 1, nullptr, ep);
         DLLM_LAUNCH_CHECK();
         return DLLM_OK;
     }
     float *ws = device_workspace(st, static_cast<size_t>(nsplit) * a.M * a.Npad * sizeof(float));
     if (!ws) return DLLM_ERR_HIP;
-    wq_gemm_exact_kernel<BITS, YT, NW, MR, SPS, KPG, true, 0, TM, 1, WREG, GPS, RING, KG, false, S16><<<nb, NW * KG * 64, 0, st>>>(
+    wq_gemm_exact_kernel<BITS, YT, NW, MR, SPS, KPG, true, 0, TM, 1, WREG, GPS, RING, KG, false, S16, STAG><<<nb, NW * KG * 64, 0, st>>>(
         a.X, a.M, a.K, a.wdev, a.sz, a.sf, a.bias, Y, a.N, a.Npad, a.group, nbm, nbn, nsplit, ws);
     DLLM_LAUNCH_CHECK();
     const size_t q = static_cast<size_t>(a.M) * (a.Npad / 4);
@@ -1020,6 +1059,11 @@ int launch_exact_bits(const ExactGemmArgs &a, hipStream_t st) {
 #endif
             return launch_exact_tile<BITS, YT, 8, 4, 2, 1, EPI>(a, 1, st);
         }
+#if DLLM_EXACT_STAG
+        // the two wave halves half a step apart (4-slot ring, stage kt + 2 issued in step kt; 136 KiB)
+        else if constexpr (G64 == 2 && BITS == 4 && DLLM_EXACT_WREG && !DLLM_EXACT_S16)
+            return launch_exact_tile<BITS, YT, 8, 4, 2, 1, EPI, false, 1, 4, 1, true, false, false, true>(a, 1, st);
+#endif
         else return launch_exact_tile<BITS, YT, 8, 4, 2, G64 / 2, EPI>(a, 1, st);
     }
     const int tiles = mb * (a.Npad / 128), ngroups = a.K / a.group;

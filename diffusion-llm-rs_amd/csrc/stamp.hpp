@@ -28,17 +28,19 @@ constexpr int kMaxStep = (kEpi - 2) / kPerStep - 1;   // steps past this are not
 }  // namespace dllm
 #define DLLM_STAMP_BUFFER(name) \
     static __device__ unsigned long long name[dllm::stamp::kBlocks * dllm::stamp::kWaves * dllm::stamp::kSlots]
+// Linear block id, so a 2-D grid (the decode kernel's K-split) does not fold rows onto each other.
+#define DLLM_STAMP_BLOCK (blockIdx.x + gridDim.x * blockIdx.y)
 #define DLLM_STAMP_ROW(buf) \
-    (buf + (static_cast<size_t>(blockIdx.x) * dllm::stamp::kWaves + (threadIdx.x >> 6)) * dllm::stamp::kSlots)
+    (buf + (static_cast<size_t>(DLLM_STAMP_BLOCK) * dllm::stamp::kWaves + (threadIdx.x >> 6)) * dllm::stamp::kSlots)
 #define DLLM_STAMP_AT(buf, slot)                                                                            \
     do {                                                                                                    \
         const int _s = (slot);                                                                              \
-        if ((threadIdx.x & 63) == 0 && blockIdx.x < dllm::stamp::kBlocks && _s >= 0 && _s < dllm::stamp::kSlots) \
+        if ((threadIdx.x & 63) == 0 && DLLM_STAMP_BLOCK < dllm::stamp::kBlocks && _s >= 0 && _s < dllm::stamp::kSlots) \
             DLLM_STAMP_ROW(buf)[_s] = __builtin_amdgcn_s_memtime();                                         \
     } while (0)
 #define DLLM_STAMP_RT(buf, slot)                                                                            \
     do {                                                                                                    \
-        if ((threadIdx.x & 63) == 0 && blockIdx.x < dllm::stamp::kBlocks)                                   \
+        if ((threadIdx.x & 63) == 0 && DLLM_STAMP_BLOCK < dllm::stamp::kBlocks)                                   \
             DLLM_STAMP_ROW(buf)[slot] = __builtin_amdgcn_s_memrealtime();                                   \
     } while (0)
 #define DLLM_STAMP_IDS(buf)                                                                                 \
@@ -46,7 +48,7 @@ constexpr int kMaxStep = (kEpi - 2) / kPerStep - 1;   // steps past this are not
         unsigned _hw, _xcc;                                                                                 \
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(_hw));                                   \
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(_xcc));                                 \
-        if ((threadIdx.x & 63) == 0 && blockIdx.x < dllm::stamp::kBlocks) {                                 \
+        if ((threadIdx.x & 63) == 0 && DLLM_STAMP_BLOCK < dllm::stamp::kBlocks) {                                 \
             DLLM_STAMP_ROW(buf)[dllm::stamp::kHwId] = _hw;                                                  \
             DLLM_STAMP_ROW(buf)[dllm::stamp::kXcc] = _xcc;                                                  \
         }                                                                                                   \
