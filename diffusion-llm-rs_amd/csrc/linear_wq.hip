@@ -809,6 +809,10 @@ wq_gemm8_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__re
 #include "lab/wq_ring256.inc"
 #endif
 
+#ifndef DLLM_DECODE_XL
+#define DLLM_DECODE_XL 1
+#endif
+
 // ---------------------------------------------------------------------------------------------
 // Decode GEMM (small M, weight-streaming / HBM-bound): one block per 16 NT-column group and
 // K-slice (grid Npad/(16 NT) x nsplit), 8 waves split the block's K-slice by 128-deep slabs,
@@ -834,7 +838,18 @@ DLLM_STAMP_BUFFER(g_stamp_dec);
 // its group(s) (group 64: two folds per 128-deep slab; group >= 128: one).  With one group per
 // slab every lane's own {zp} dword is already its column's for all four 32-deep steps, so EXACT = 2
 // skips the per-step ds_bpermute (an LDS round trip on the dequant's critical path).
-template <int BITS, typename YT, int MT, int NT = 1, bool SPLIT = false, int LAB = 0, int EXACT = 0, int DW = kDecWaves>
+// XL (M <= 16, NT = 1, EXACT = 2, one K-slice, every wave owning a slab): the block's X rows
+// [M][K], one zero row and its columns' zero-point pairs and scales for every group are staged once
+// in LDS (dynamic, xl_lds_bytes) by LDS-DMA -- 1 KiB per instruction -- instead of each wave
+// fetching its own 16-B fragments per slab.  At M = 1 fifteen of sixteen fragment lanes were out of
+// range and the scales were 4-16x redundant: 224 vector-memory instructions per CU for 32 KiB of
+// weight words, which bounded the decode layer by the per-CU load issue rate, not by HBM
+// (profiles/r05_midm).  With XL a CU issues the 32 weight loads, 8 X chunks and 16 scale rows --
+// which measured no faster at M <= 8 (the layer waits on the weight stream's latency, not on load
+// issue), and 7 % faster at M = 16, where the 16 lanes of a fragment are all in range; the product
+// uses it for M 9..16.
+template <int BITS, typename YT, int MT, int NT = 1, bool SPLIT = false, int LAB = 0, int EXACT = 0, int DW = kDecWaves,
+          bool XL = false>
 __global__ void __launch_bounds__(DW * 64)
 wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdec,
                  const uint32_t *__restrict__ sz, const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad,
@@ -883,6 +898,41 @@ wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
         bv[nt] = SPLIT ? float4{0.f, 0.f, 0.f, 0.f}
                        : *reinterpret_cast<const float4 *>(bias + n0 + 16 * nt + 4 * (lane >> 4));
 
+    static_assert(!XL || (MT == 1 && NT == 1 && EXACT == 2 && !SPLIT && LAB == 0), "XL: M <= 16, one tile, group >= 128");
+    extern __shared__ __attribute__((aligned(16))) uint8_t xl_lds[];
+    const int xl_pitch = K * 2 + 16;   // rows 16 B apart in bank order: the 16 rows of a fragment read hit 64 banks
+    uint32_t xl_row = 0, xl_zero = 0;  // XL: this lane's fragment base (its token row, or the zero row)
+    int xl_sz = 0, xl_sf = 0;          // XL: LDS offsets of the zero-point pair rows and the scale rows
+    if constexpr (XL) {
+        auto u = [](uint32_t v) { return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(v))); };
+        const uint32_t base = lds_addr(xl_lds);
+        const int cpr = K / 512;   // 1-KiB chunks per X row
+        for (int c = wave; c < M * cpr; c += DW) {
+            const int row = c / cpr, cc = c - row * cpr;
+            blds16_asm(xrs, static_cast<uint32_t>(lane * 16), u(static_cast<uint32_t>((row * K + cc * 512) * 2)),
+                       u(base + static_cast<uint32_t>(row * xl_pitch + cc * 1024)));
+        }
+        // zero-point pairs then scales: ng rows of the block's 16 columns; one DMA moves 4 rows
+        const int ng = K / group, nq = (ng + 3) / 4;
+        xl_sz = (M + 1) * xl_pitch;
+        xl_sf = xl_sz + nq * 256;
+        const uint32_t pv = static_cast<uint32_t>(((lane >> 4) * Npad + (lane & 15)) * 4);
+        const uint32_t prange = static_cast<uint32_t>((static_cast<size_t>(ng) * Npad - n0) * 4);
+        const __amdgpu_buffer_rsrc_t szr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(sz + n0), 0, static_cast<int>(prange), 0x00020000);
+        const __amdgpu_buffer_rsrc_t sfr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(sf + n0), 0, static_cast<int>(prange), 0x00020000);
+        for (int q = wave; q < 2 * nq; q += DW) {
+            const int j = q >> 1;
+            const uint32_t dst = u(base + static_cast<uint32_t>(((q & 1) ? xl_sf : xl_sz) + j * 256));
+            const uint32_t so = u(static_cast<uint32_t>(4 * j * Npad * 4));
+            if (q & 1) blds4_asm(sfr, pv, so, dst);
+            else blds4_asm(szr, pv, so, dst);
+        }
+        for (int c = tid; c < K / 8; c += DW * 64)
+            *reinterpret_cast<uint4 *>(xl_lds + M * xl_pitch + c * 16) = uint4{0u, 0u, 0u, 0u};
+        xl_zero = static_cast<uint32_t>(M * xl_pitch + 16 * (lane >> 4));
+        xl_row = (lane & 15) < M ? static_cast<uint32_t>((lane & 15) * xl_pitch + 16 * (lane >> 4)) : xl_zero;
+    }
+
     float4_t acc[NT][MT];
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
@@ -909,6 +959,7 @@ wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
                 } else {
                     load_words<BITS>(w[i][nt], wbase + nt * wtile + static_cast<size_t>(slab) * 64 * BITS);
                 }
+                if constexpr (XL) continue;   // scales from LDS below
                 if constexpr (LAB & 2) szl[i][nt] = 0x3c00e400u + ks;
                 else szl[i][nt] = szcol[static_cast<size_t>(ks / group) * Npad + 16 * nt];
                 if constexpr (EXACT) {
@@ -919,6 +970,7 @@ wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
                     sfl[i][nt][1] = *reinterpret_cast<const float4 *>(sf + static_cast<size_t>(g1) * Npad + nb0);
                 }
             }
+            if constexpr (XL) continue;   // X fragments from LDS below
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
                 const int k = slab_raw * 128 + t * 32;
@@ -938,6 +990,27 @@ wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
         // Keep the scheduler from sinking the loads back next to their MFMAs (it does so to cut
         // register pressure, which turns the round into one serial latency per fragment).
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (XL) {
+            if (round == 0) {
+                // The block's LDS-DMAs precede this round's weight loads (at least kDepth
+                // instructions; the DMAs are older), so this count waits for the DMAs only.
+                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kDepth * (BITS == 8 ? 2 : 1)) : "memory");
+                __builtin_amdgcn_s_barrier();
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int i = 0; i < kDepth; ++i) {
+                const int slab_raw = base + i * DW;
+                const int slab = min(slab_raw, s_end - 1);
+                const uint32_t lb = (slab_raw < s_end ? xl_row : xl_zero) + static_cast<uint32_t>(slab * 256);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) xb[i][t][0] = *reinterpret_cast<const half8_t *>(xl_lds + lb + t * 64);
+                const int g = (slab * 128) / group;
+                szl[i][0] = *reinterpret_cast<const uint32_t *>(xl_lds + xl_sz + (g * 16 + (lane & 15)) * 4);
+                sfl[i][0][0] = sfl[i][0][1] =
+                    *reinterpret_cast<const float4 *>(xl_lds + xl_sf + (g * 16 + 4 * (lane >> 4)) * 4);
+            }
+        }
         DLLM_STAMP_AT(g_stamp_dec, round < 20 ? 1 + 2 * round : -1);
         if constexpr (EXACT) {
 #pragma unroll
@@ -1039,6 +1112,14 @@ namespace {
 
 constexpr int kDecodeMaxM = 64;
 
+// XL decode (M <= 16): dynamic LDS of X rows + zero row (2K + 16 B each) + pair and scale rows
+// (256 B per 4 groups each), within the CU's 160 KiB beside the 8 KiB partial-sum buffer.
+constexpr size_t kXlLdsMax = 160 * 1024 - kDecWaves * 64 * 4 * 4;
+inline size_t xl_lds_bytes(int M, int K, int group) {
+    const size_t nq = static_cast<size_t>((K / group + 3) / 4);
+    return static_cast<size_t>(M + 1) * (2 * static_cast<size_t>(K) + 16) + 2 * nq * 256;
+}
+
 // Exact-weight kernels apply when the group tiles K (a stage never straddles two groups).
 inline bool use_exact(const dllm_linear *h) {
     return h->precision == DLLM_PRECISION_EXACT &&
@@ -1063,6 +1144,25 @@ int launch_decode_nt(const dllm_linear *h, const __half *X, int M, YT *Y, int ns
     const int nslab = (K + 127) / 128;
     nsplit = std::max(1, std::min(nsplit, nslab));
     if (nsplit == 1) {
+#if DLLM_DECODE_XL
+        if constexpr (MT == 1 && NT == 1 && EXACT == 2) {
+            const size_t bytes = xl_lds_bytes(M, K, gr);
+            // M 9..16 only: M = 16 6.75 vs 7.25 us per layer in the 40-layer chain, M = 1 / 2 / 4 / 8
+            // 5.16 / 5.34 / 5.58 / 6.00 vs 5.18 / 5.38 / 5.47 / 5.94 (profiles/r05_decode_xl/): fewer
+            // load instructions do not shorten the M <= 8 layer, whose time is the weight stream's
+            // latency, and the DMA wait + barrier before the first MFMA costs a little there.
+            if (M > 8 && K % 512 == 0 && nslab >= kDecWaves && bytes <= kXlLdsMax) {
+                auto *kern = &wq_decode_kernel<BITS, YT, 1, 1, false, 0, 2, kDecWaves, true>;
+                static const bool attr_ok = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                                static_cast<int>(kXlLdsMax)) == hipSuccess;
+                if (!attr_ok) return fail(DLLM_ERR_HIP, "decode XL LDS attribute");
+                kern<<<nbx, kDecWaves * 64, bytes, st>>>(X, M, K, h->wdec, h->sz, h->bias, Y, N, Np, gr, 1, nullptr, h->sf);
+                DLLM_LAUNCH_CHECK();
+                return DLLM_OK;
+            }
+        }
+#endif
 #if DLLM_LAB
         if constexpr (MT * NT <= 2) {
             if (h->variant == 306) {   // lab A/B: 16 waves per block (two slabs each at K = 4096)
