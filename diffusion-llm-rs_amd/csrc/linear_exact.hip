@@ -56,7 +56,8 @@
 // DLLM_EXACT_STAG = 1: the 128 x 256 int4 g128 tiles run their two wave halves half a step apart
 // (M 2048 / 3072 x 4096: 76.9 -> 73.9 / 121.6 -> 114.0 us, same bits).  The k-group tiles with
 // their k-group halves staggered measured 2-7 % slower (4096 x 1024 / 512, 256 / 512 x 4096) and
-// stay unstaggered (profiles/r05_stag).
+// stay unstaggered, and the staggered tiles on 16x16x32 MFMAs measured within +-1.5 % (mixed
+// sign) of these (profiles/r05_stag).
 #ifndef DLLM_EXACT_STAG
 #define DLLM_EXACT_STAG 1
 #endif
@@ -263,7 +264,7 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
     static_assert(RING == 3 || (RING >= 2 && RING <= 8 && !TM), "ring depth");
     static_assert(KG == 1 || (!TM && RING * KG * SL::kBytes >= (KG - 1) * NW * 64 * MR * 16 * 4), "k-group combine fits the ring");
     static_assert(!S16 || (!TM && !HORN), "16x16x32 form: fold kernels");
-    static_assert(!STAG || (!TM && !HORN && !S16 && GPS == 1 && (KG == 1 ? RING >= 4 && NW % 2 == 0 : KG % 2 == 0)),
+    static_assert(!STAG || (!TM && !HORN && GPS == 1 && (KG == 1 ? RING >= 4 && NW % 2 == 0 : KG % 2 == 0)),
                   "staggered halves");
     // Stage kt + kDist is issued at the head of step kt.  STAG: one half of the block's waves runs
     // half a step behind the other (one extra barrier at entry; the early half one at exit; a
@@ -648,24 +649,25 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
             if constexpr (DLLM_EXACT_PRIO) __builtin_amdgcn_s_setprio(0);
             __builtin_amdgcn_sched_barrier(0);
         };
+        // STAG: the mid-step barrier (the other half's step boundary).  The late half's share of
+        // stage kt + 1 must land before it: the early half starts reading kt + 1 right after.
+        auto mid = [&]() __attribute__((always_inline)) {
+            if constexpr (STAG) {
+                if (wait_mid) {
+                    if (issue) wait_prev();
+                    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                __builtin_amdgcn_s_barrier();
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        };
         if constexpr (S16) {
             [&]<int... Vs>(std::integer_sequence<int, Vs...>) __attribute__((always_inline)) {
                 ((Vs % 2 == 0 ? sub16(bA, bB, std::integral_constant<int, Vs>{})
-                              : sub16(bB, bA, std::integral_constant<int, Vs>{})), ...);
+                              : sub16(bB, bA, std::integral_constant<int, Vs>{}),
+                  Vs == kSub / 2 - 1 ? mid() : void()), ...);
             }(std::make_integer_sequence<int, kSub>{});
         } else {
-            // STAG: the mid-step barrier (the other half's step boundary).  The late half's share of
-            // stage kt + 1 must land before it: the early half starts reading kt + 1 right after.
-            auto mid = [&]() __attribute__((always_inline)) {
-                if constexpr (STAG) {
-                    if (wait_mid) {
-                        if (issue) wait_prev();
-                        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    }
-                    __builtin_amdgcn_s_barrier();
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            };
             [&]<int... Vs>(std::integer_sequence<int, Vs...>) __attribute__((always_inline)) {
                 ((Vs % 2 == 0 ? sub(bA, bB, aA, aB, std::integral_constant<int, Vs>{})
                               : sub(bB, bA, aB, aA, std::integral_constant<int, Vs>{}),
