@@ -918,15 +918,21 @@ wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
         xl_sf = xl_sz + nq * 256;
         const uint32_t pv = static_cast<uint32_t>(((lane >> 4) * Npad + (lane & 15)) * 4);
         const uint32_t prange = static_cast<uint32_t>((static_cast<size_t>(ng) * Npad - n0) * 4);
-        const __amdgpu_buffer_rsrc_t szr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(sz + n0), 0, static_cast<int>(prange), 0x00020000);
-        const __amdgpu_buffer_rsrc_t sfr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(sf + n0), 0, static_cast<int>(prange), 0x00020000);
-        for (int q = wave; q < 2 * nq; q += DW) {
-            const int j = q >> 1;
-            const uint32_t dst = u(base + static_cast<uint32_t>(((q & 1) ? xl_sf : xl_sz) + j * 256));
-            const uint32_t so = u(static_cast<uint32_t>(4 * j * Npad * 4));
-            if (q & 1) blds4_asm(sfr, pv, so, dst);
-            else blds4_asm(szr, pv, so, dst);
-        }
+        // descriptor fields through readfirstlane: the asm's "s" operand needs them provably uniform
+        auto uptr = [](const void *p) {
+            const uint64_t v = reinterpret_cast<uint64_t>(p);
+            const uint64_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(v)));
+            const uint64_t hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(v >> 32)));
+            return reinterpret_cast<void *>((hi << 32) | lo);
+        };
+        const int pr = __builtin_amdgcn_readfirstlane(static_cast<int>(prange));
+        const __amdgpu_buffer_rsrc_t szr = __builtin_amdgcn_make_buffer_rsrc(uptr(sz + n0), 0, pr, 0x00020000);
+        const __amdgpu_buffer_rsrc_t sfr = __builtin_amdgcn_make_buffer_rsrc(uptr(sf + n0), 0, pr, 0x00020000);
+        // (two loops, one descriptor each: a select between them is not provably uniform)
+        for (int j = wave; j < nq; j += DW)
+            blds4_asm(szr, pv, u(static_cast<uint32_t>(4 * j * Npad * 4)), u(base + static_cast<uint32_t>(xl_sz + j * 256)));
+        for (int j = wave; j < nq; j += DW)
+            blds4_asm(sfr, pv, u(static_cast<uint32_t>(4 * j * Npad * 4)), u(base + static_cast<uint32_t>(xl_sf + j * 256)));
         for (int c = tid; c < K / 8; c += DW * 64)
             *reinterpret_cast<uint4 *>(xl_lds + M * xl_pitch + c * 16) = uint4{0u, 0u, 0u, 0u};
         xl_zero = static_cast<uint32_t>(M * xl_pitch + 16 * (lane >> 4));

@@ -900,6 +900,33 @@ def test_gemm_variants_bit_identical(dllm, torch):
     assert torch.equal(outs[8], outs[11]) and torch.equal(outs16[8], outs16[11])
 
 
+@pytest.mark.parametrize("bits", [2, 4, 8])
+def test_linear_decode_lds_staged_exact_integers(dllm, torch, bits):
+    """The decode path for M 9..16 (linear_wq.hip, XL: the block's X rows, a zero row and its
+    columns' zero-point pairs / scales staged in LDS) on exact-integer data, product policy: every
+    partial is exact, so each output equals the f64 product bit for bit.  Shapes: K 1536 (12 slabs
+    over 8 waves: clamped duplicate slabs read the zero row), K 6144 (two rounds of slabs), group
+    256, a padded last column group (N 200 / 136), and M 8 / 17 on either side of the XL range."""
+    for K, N, group, Ms in ((1024, 200, 128, (8, 9, 16, 17)), (1536, 136, 128, (12,)),
+                            (6144, 64, 128, (9,)), (4096, 256, 256, (16,))):
+        rng = np.random.default_rng(7 * bits + K)
+        q = (1 << bits) - 1
+        W = rng.integers(0, q + 1, (K, N)).astype(np.float32)
+        for g0 in range(0, K, group):
+            W[g0, :], W[g0 + 1, :] = 0.0, float(q)
+        b = rng.integers(-4, 5, N).astype(np.float32)
+        lin = dllm.QuantLinear.from_weight(dev(torch, W), dev(torch, b), bits, group)
+        for M in Ms:
+            X = rng.integers(-2, 3, (M, K)).astype(np.float32)
+            ref = (X.astype(np.float64) @ W.astype(np.float64) + b).astype(np.float32)
+            Xd = dev(torch, X).half()
+            assert np.array_equal(host(lin(Xd, out_dtype=torch.float32)), ref), (bits, K, N, group, M)
+            if np.abs(ref).max() < 60000:
+                Y16 = host(lin(Xd, out_dtype=torch.float16).float())
+                assert np.array_equal(Y16, ref.astype(np.float16).astype(np.float32)), (bits, K, M, "f16")
+        lin.close()
+
+
 @pytest.mark.lab
 @pytest.mark.parametrize("bits", [2, 4, 8])
 def test_linear_decode_tiles_exact_integers(dllm, torch, orc, bits):
