@@ -250,6 +250,14 @@ __device__ __forceinline__ float swap_halves_sum(float x) {
 // of its R1(kb) (V(kb - 1) last read by B in 2 kb) and waits for it before the barrier ending
 // interval 2 kb + 2 (first read by A in 2 kb + 5).  Same arithmetic per query as STAG = false:
 // the outputs are bit-identical.
+// DLLM_ATTN_BDMA = 1: K / V staging through a buffer descriptor with compile-time pieces (C4: 1.005
+// -> 0.971 ms and 1.037 -> 1.017 ms on two boxes, bit-identical; a one-M0-save burst of the two
+// whole rounds measured slower than this, profiles/r05_bdma/).
+#ifndef DLLM_ATTN_BDMA
+#define DLLM_ATTN_BDMA 1
+#endif
+constexpr bool kAttnBdma = DLLM_ATTN_BDMA != 0;
+
 template <int LAB = 0, bool STAG = false>
 __global__ void __launch_bounds__(kWaves * 64)
 kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__ img, const float *__restrict__ kp,
@@ -300,14 +308,36 @@ kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__
     const uint8_t *himg = img + static_cast<size_t>(h) * nkb * kImg + lane * 16;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(wave);
     // pieces p0, p0 + step, ... of an image (the whole workgroup: wv, 8; one group: wv % 4, 4)
+    // BDMA: the whole-workgroup form through a buffer descriptor of the head's images -- the block
+    // and piece in the scalar offset, one fixed per-lane offset, the pieces unrolled at compile time
+    // -- instead of a run-time loop of global_load_lds with a 64-bit address add per piece.
+    const __amdgpu_buffer_rsrc_t irs = raw_rsrc(img + static_cast<size_t>(h) * nkb * kImg);
+    auto u = [](uint32_t v) { return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(v))); };
+    auto dma_b = [&](uint32_t off0, uint32_t dst0, auto n_tag) __attribute__((always_inline)) {
+        constexpr int n = decltype(n_tag)::value;
+#pragma unroll
+        for (int i = 0; i < (n + kWaves - 1) / kWaves; ++i) {
+            const uint32_t p = wv + kWaves * i;
+            if ((i + 1) * kWaves <= n || p < static_cast<uint32_t>(n))
+                blds16_asm(irs, static_cast<uint32_t>(lane * 16), u(off0 + p * 1024), u(dst0 + p * 1024));
+        }
+    };
     auto dma_k = [&](int blk, int buf, uint32_t p0 = 0xffffffffu, uint32_t step = kWaves) {
-        const uint8_t *src = himg + static_cast<size_t>(blk) * kImg;
         const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_addr(&sm.k[buf][0][0]));
+        if (kAttnBdma && p0 == 0xffffffffu && step == kWaves) {
+            dma_b(static_cast<uint32_t>(blk * kImg), dst, std::integral_constant<int, kKImg / 1024>{});
+            return;
+        }
+        const uint8_t *src = himg + static_cast<size_t>(blk) * kImg;
         for (uint32_t p = p0 == 0xffffffffu ? wv : p0; p < kKImg / 1024; p += step) glds16_asm(src + p * 1024, dst + p * 1024);
     };
     auto dma_v = [&](int blk, int buf, uint32_t p0 = 0xffffffffu, uint32_t step = kWaves) {
-        const uint8_t *src = himg + static_cast<size_t>(blk) * kImg + kKImg;
         const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_addr(&sm.vt[buf][0][0]));
+        if (kAttnBdma && p0 == 0xffffffffu && step == kWaves) {
+            dma_b(static_cast<uint32_t>(blk * kImg + kKImg), dst, std::integral_constant<int, kVImg / 1024>{});
+            return;
+        }
+        const uint8_t *src = himg + static_cast<size_t>(blk) * kImg + kKImg;
         for (uint32_t p = p0 == 0xffffffffu ? wv : p0; p < kVImg / 1024; p += step) glds16_asm(src + p * 1024, dst + p * 1024);
     };
     const bool grp_b = STAG && wave >= kWaves / 2;
