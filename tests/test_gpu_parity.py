@@ -900,6 +900,31 @@ def test_gemm_variants_bit_identical(dllm, torch):
     assert torch.equal(outs[8], outs[11]) and torch.equal(outs16[8], outs16[11])
 
 
+@pytest.mark.parametrize("K", [128, 256, 384, 1152])
+def test_linear_staggered_tiles_exact_integers(dllm, torch, K):
+    """The 128 x 256 exact fold tiles with staggered wave halves (linear_exact.hip, DLLM_EXACT_STAG:
+    a 4-slot ring, stage kt + 2 issued in step kt, the late half's share of stage kt + 1 awaited at
+    the mid-step barrier), product policy, on exact-integer data: every partial is exact, so each
+    output equals the f64 product bit for bit.  M 2048 / 2100 x N 4096 take those tiles (>= 256 of
+    them; 2100 leaves a ragged last row block); K 128 / 256 / 384 run fewer stages than the ring
+    keeps in flight (1 / 2 / 3), K 1152 a ring period that does not divide the stage count."""
+    N = 4096
+    rng = np.random.default_rng(K)
+    W = rng.integers(0, 16, (K, N)).astype(np.float32)
+    for g0 in range(0, K, 128):
+        W[g0, :], W[g0 + 1, :] = 0.0, 15.0
+    b = rng.integers(-4, 5, N).astype(np.float32)
+    lin = dllm.QuantLinear.from_weight(dev(torch, W), dev(torch, b), 4, 128, prefill_only=True)
+    for M in (2048, 2100):
+        X = rng.integers(-2, 3, (M, K)).astype(np.float32)
+        ref = (X.astype(np.float64) @ W.astype(np.float64) + b).astype(np.float32)
+        Xd = dev(torch, X).half()
+        assert np.array_equal(host(lin(Xd, out_dtype=torch.float32)), ref), (K, M)
+        Y16 = host(lin(Xd, out_dtype=torch.float16).float())
+        assert np.array_equal(Y16, ref.astype(np.float16).astype(np.float32)), (K, M, "f16")
+    lin.close()
+
+
 @pytest.mark.parametrize("bits", [2, 4, 8])
 def test_linear_decode_lds_staged_exact_integers(dllm, torch, bits):
     """The decode path for M 9..16 (linear_wq.hip, XL: the block's X rows, a zero row and its
