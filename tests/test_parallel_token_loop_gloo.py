@@ -1,4 +1,4 @@
-"""CPU multi-process test (gloo, world_size 2) of config C5 token-parallel (SURVEY.md 8e's
+"""CPU multi-process test (gloo, world_size 2 and 3 -- 3 splits the rows unevenly) of config C5 token-parallel (SURVEY.md 8e's
 exchange-free alternative): ``DenoiseLoop`` (DiffuseLLM::sample, diffuse-llm-rs/src/lib.rs:853-955)
 on every rank over ITS token rows of x (``parallel.token_rows``) through replicated layers -- the
 linear layers (lib.rs:806-813) and p_sample (:1152-1215) are per token, so no collective -- with
@@ -27,9 +27,6 @@ if str(ROOT) not in sys.path:
 from tests.test_parallel_gloo import OracleLinear  # noqa: E402
 from tests.test_parallel_loop_gloo import (D, HD, HEADS, SEQ, SEED, STEPS, OracleKVOps,  # noqa: E402
                                            OracleLoopOps, _cfg, _free_port, _inputs, _unsharded)
-
-WORLD = 2
-
 
 def _worker(rank, world, port, outdir):
     sys.path.insert(0, str(ROOT))
@@ -68,11 +65,12 @@ def _worker(rank, world, port, outdir):
     dist.destroy_process_group()
 
 
-@pytest.fixture(scope="module")
-def results(tmp_path_factory):
-    out = tmp_path_factory.mktemp("tokloop")
-    mp.spawn(_worker, args=(WORLD, _free_port(), str(out)), nprocs=WORLD, join=True)
-    return [dict(np.load(out / f"rank{r}.npz")) for r in range(WORLD)]
+@pytest.fixture(scope="module", params=[2, 3])
+def results(request, tmp_path_factory):
+    world = request.param
+    out = tmp_path_factory.mktemp(f"tokloop{world}")
+    mp.spawn(_worker, args=(world, _free_port(), str(out)), nprocs=world, join=True)
+    return [dict(np.load(out / f"rank{r}.npz")) for r in range(world)]
 
 
 @pytest.fixture(scope="module")
