@@ -40,6 +40,7 @@
 #endif
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <map>
 #include <tuple>
@@ -1159,10 +1160,18 @@ int launch_decode_nt(const dllm_linear *h, const __half *X, int M, YT *Y, int ns
             // latency, and the DMA wait + barrier before the first MFMA costs a little there.
             if (M > 8 && K % 512 == 0 && nslab >= kDecWaves && bytes <= kXlLdsMax) {
                 auto *kern = &wq_decode_kernel<BITS, YT, 1, 1, false, 0, 2, kDecWaves, true>;
-                static const bool attr_ok = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                                                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                                static_cast<int>(kXlLdsMax)) == hipSuccess;
-                if (!attr_ok) return fail(DLLM_ERR_HIP, "decode XL LDS attribute");
+                // the dynamic-LDS limit, set once per device (a bit per device id; a process may drive
+                // several GPUs)
+                static std::atomic<uint64_t> attr_set{0};
+                int dev = 0;
+                if (hipGetDevice(&dev) != hipSuccess) return fail(DLLM_ERR_HIP, "decode XL device");
+                const uint64_t bit = dev < 64 ? (uint64_t{1} << dev) : 0;
+                if (!bit || !(attr_set.load(std::memory_order_acquire) & bit)) {
+                    if (hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            static_cast<int>(kXlLdsMax)) != hipSuccess)
+                        return fail(DLLM_ERR_HIP, "decode XL LDS attribute");
+                    attr_set.fetch_or(bit, std::memory_order_acq_rel);
+                }
                 kern<<<nbx, kDecWaves * 64, bytes, st>>>(X, M, K, h->wdec, h->sz, h->bias, Y, N, Np, gr, 1, nullptr, h->sf);
                 DLLM_LAUNCH_CHECK();
                 return DLLM_OK;
