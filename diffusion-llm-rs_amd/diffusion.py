@@ -443,6 +443,11 @@ class DenoiseLoop:
         self._betas = config.create_beta_schedule()
         self._coef_cache = {}
         self._side = None
+        # kv_spread: the side stream's KV step i waits for the main stream to reach step i, so the
+        # 50 KV steps run beside their own steps instead of back to back from the start (config C5:
+        # 0.861 -> 0.841 ms per step, median of 6 rounds, and a tighter spread; bit-identical;
+        # profiles/r05_spread/).  False: the round-4 free-running side stream.
+        self.kv_spread = True
         self._noise = None
 
     def _coef(self, t: int) -> tuple[torch.Tensor, bool]:
@@ -549,6 +554,8 @@ class DenoiseLoop:
             out16 = None if f16 is None else f16[(i + 1) % 2]
             if self.noise_mode == "epilogue":      # noise drawn in the last layer's epilogue
                 with torch.cuda.stream(side):
+                    if self.kv_spread:             # KV step i starts with step i (see __init__)
+                        side.wait_stream(main)
                     self.kv_step(t, num_steps)
                 buf = self.step(x, t, i, out=buf, x16=x16, out16=out16)
                 x, buf = buf, x

@@ -24,13 +24,14 @@ K0 = torch.randn(1, M, dm, device=dev, generator=gen)
 V0 = torch.randn(1, M, dm, device=dev, generator=gen)
 x = torch.randn(M, dm, device=dev, generator=gen)
 modes = {"product": dict(overlap=True), "serial": dict(overlap=False), "nokv": dict(overlap=True),
-         "product_cast": dict(overlap=True)}   # product_cast: without the f16 x_prev hand-off
+         "product_cast": dict(overlap=True), "spread": dict(overlap=True)}   # product_cast: without the f16 x_prev hand-off
 res = {}
 for rnd in range(int(__import__("os").environ.get("ROUNDS", "2"))):
     for name in want:
         kv = None if name == "nokv" else d.KVCacheEntry.new(K0.clone(), V0.clone(), cfg.prefill_bits, cfg.decode_bits)
         loop = d.DenoiseLoop(layers, cfg, cumprod=d.Cumprod.INCLUSIVE, seed=1, kv_cache=kv, **modes[name])
         loop.f16_handoff = name != "product_cast"
+        loop.kv_spread = name != "product"     # "product": the round-4 free-running side stream
         loop.sample(x, 3)
         torch.cuda.synchronize()
         st = torch.cuda.current_stream()
