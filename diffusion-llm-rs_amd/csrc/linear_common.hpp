@@ -28,6 +28,36 @@ namespace {
 
 constexpr int kBM = 256, kBN = 128, kBK = 64, kThreads = 256;
 
+// Four consecutive outputs (element i = m N + n .. + 3) of the fused epilogue with x_t[i..i+3] and
+// the row's coefficients already loaded: a caller that hoists every tile load above the tile's
+// stores keeps them off the per-group path (x_prev may alias x_t / coef as far as the compiler can
+// prove, so loads issued per group wait behind the previous group's stores).  N % 4 == 0,
+// offset % 4 == 0.
+__device__ __forceinline__ void psample4_x(const PSampleEpi &e, size_t i, float4 x, float c1, float c2, float sd,
+                                           float e0, float e1, float e2, float e3) {
+    float z[4] = {0.f, 0.f, 0.f, 0.f};
+    if (e.add) {
+        if (e.noise) {
+            const float4 nv = *reinterpret_cast<const float4 *>(e.noise + i);
+            z[0] = nv.x; z[1] = nv.y; z[2] = nv.z; z[3] = nv.w;
+        } else {
+            rng::normal4(e.seed, (e.offset + i) / 4, z);
+        }
+    }
+    float4 o;
+    o.x = (c1 * x.x + c2 * e0) + sd * z[0];
+    o.y = (c1 * x.y + c2 * e1) + sd * z[1];
+    o.z = (c1 * x.z + c2 * e2) + sd * z[2];
+    o.w = (c1 * x.w + c2 * e3) + sd * z[3];
+    *reinterpret_cast<float4 *>(e.x_prev + i) = o;
+    if (e.x_prev_h) {
+        union { __half h[4]; uint2 u; } pk;
+        pk.h[0] = __float2half_rn(o.x); pk.h[1] = __float2half_rn(o.y);
+        pk.h[2] = __float2half_rn(o.z); pk.h[3] = __float2half_rn(o.w);
+        *reinterpret_cast<uint2 *>(e.x_prev_h + i) = pk.u;
+    }
+}
+
 // Four consecutive outputs (m, n..n+3) of the fused epilogue; N % 4 == 0, offset % 4 == 0.
 __device__ __forceinline__ void psample4(const PSampleEpi &e, int m, int n, int N, float e0, float e1, float e2,
                                          float e3) {

@@ -944,6 +944,22 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
     #pragma unroll
         for (int qd = 0; qd < 4; ++qd) bv[qd] = *reinterpret_cast<const float4 *>(bias + nb0 + 8 * qd);
         if constexpr (EPI == 1) {
+            // every x_t value and row coefficient of the tile is loaded before the first store (see
+            // psample4_x): one memory round trip for the tile instead of two per 4-column group
+            float4 xt[MR][4];
+            float cf[MR][3];
+    #pragma unroll
+            for (int r = 0; r < MR; ++r) {
+                const int m = m0 + r * 32 + (lane & 31);
+                const bool mok = m < M;
+                const float *c = epi.coef + 3 * ((mok ? m : 0) / epi.rps);
+                cf[r][0] = c[0]; cf[r][1] = c[1]; cf[r][2] = c[2];
+    #pragma unroll
+                for (int qd = 0; qd < 4; ++qd)
+                    xt[r][qd] = mok && nb0 + 8 * qd < N
+                                    ? *reinterpret_cast<const float4 *>(epi.x_t + static_cast<size_t>(m) * N + nb0 + 8 * qd)
+                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
     #pragma unroll
             for (int r = 0; r < MR; ++r) {
                 const int m = m0 + r * 32 + (lane & 31);
@@ -951,8 +967,9 @@ wq_gemm_exact_kernel(const __half *__restrict__ X, int M, int K, const uint32_t 
     #pragma unroll
                 for (int qd = 0; qd < 4; ++qd) {
                     if (nb0 + 8 * qd >= N) continue;
-                    psample4(epi, m, nb0 + 8 * qd, N, acc[r][4 * qd + 0] + bv[qd].x, acc[r][4 * qd + 1] + bv[qd].y,
-                             acc[r][4 * qd + 2] + bv[qd].z, acc[r][4 * qd + 3] + bv[qd].w);
+                    psample4_x(epi, static_cast<size_t>(m) * N + nb0 + 8 * qd, xt[r][qd], cf[r][0], cf[r][1], cf[r][2],
+                               acc[r][4 * qd + 0] + bv[qd].x, acc[r][4 * qd + 1] + bv[qd].y,
+                               acc[r][4 * qd + 2] + bv[qd].z, acc[r][4 * qd + 3] + bv[qd].w);
                 }
             }
             return;
