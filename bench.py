@@ -12,13 +12,14 @@ Multi-GPU (--gpus N, one process per GPU: launched by torch.distributed.run, or 
 is unset -- by bench.py itself, which starts N fresh rank processes before anything touches the
 GPU; a WORLD_SIZE that differs from --gpus is an error): the SAME fixed
 4096-token step is split over the ranks by hidden (output) dimension -- column-parallel, rank r
-owns the group-aligned columns [n0, n1) of W (parallel.ColumnParallelLinear), X replicated --
-so ``value`` = 4096 tokens per step / max-over-ranks step time ("scaling": "strong").  No
-collective on that data path (a Megatron column layer hands its Y slice to the row-parallel
-layer after it); the all-gather of the full Y, for a caller that needs it, is timed separately
-(``with_allgather``).  Token-parallel replicas (each rank its own 4096 tokens) are a side key
-(``replicas``, weak scaling), config C5 hidden-dim sharded over RCCL is ``denoise_loop_tp`` and C5
-token-parallel (each rank its 2048 / N tokens of the sample, replicated weights) ``denoise_loop_dp``.
+owns the group-aligned columns [n0, n1) of W (parallel.ColumnParallelLinear), X replicated -- and
+the step ends with the full [M, N] Y on every rank, as x.dot(W) + b returns it (lib.rs:812): the
+rank's slice GEMM + one RCCL all-gather of the f16 slices (``forward_gathered``).  ``value`` =
+4096 tokens per step / max-over-ranks time of that whole step ("scaling": "strong", ``value_from``
+says so); the slice GEMM alone is the side key ``kernel_only``.  Token-parallel replicas (each
+rank its own 4096 tokens) are a side key (``replicas``, weak scaling), config C5 hidden-dim
+sharded over RCCL is ``denoise_loop_tp`` and C5 token-parallel (each rank its 2048 / N tokens of
+the sample, replicated weights) ``denoise_loop_dp``.
 """
 from __future__ import annotations
 
@@ -59,16 +60,22 @@ def parse():
     p.add_argument("--sweep", action="store_true", help="rank 0 at N = 1: add the local layer's M-sweep (m_sweep) to the JSON line")
     p.add_argument("--tp-steps", type=int, default=10,
                    help="N > 1: steps of the hidden-dim-sharded C5 loop reported as 'denoise_loop_tp' (0 skips)")
+    p.add_argument("--dp-steps", type=int, default=50,
+                   help="N > 1: steps of the token-parallel C5 loop reported as 'denoise_loop_dp' (0 skips)")
+    p.add_argument("--gather-chunks", type=int, default=1,
+                   help="N > 1: token chunks of the headline step's all-gather (chunk i's gather overlaps "
+                        "chunk i+1's GEMM)")
     p.add_argument("--no-denoise", action="store_true",
                    help="skip the config-C5 denoise-loop side measurement (reported as 'denoise_loop')")
     p.add_argument("--prewarm-ms", type=float, default=300.0,
                    help="untimed launches of the same step before the W warmup steps, so the clocks "
                         "have ramped before timing (outside the timed region)")
     a = p.parse_args()
-    if a.tp_steps == 1:
-        # a 1-step schedule is the reference's degenerate linear schedule (0/0 in the beta ramp,
-        # lib.rs:554-593): its output is NaN by construction, so it measures nothing useful
-        p.error("--tp-steps must be 0 (skip) or >= 2")
+    for name in ("tp_steps", "dp_steps"):
+        if getattr(a, name) == 1:
+            # a 1-step schedule is the reference's degenerate linear schedule (0/0 in the beta ramp,
+            # lib.rs:554-593): its output is NaN by construction, so it measures nothing useful
+            p.error(f"--{name.replace('_', '-')} must be 0 (skip) or >= 2")
     return a
 
 
@@ -250,7 +257,7 @@ def denoise_loop_tp(d, torch, dist, dev, world, steps):
     res = {"workload": f"C5 hidden-dim sharded: {L // 2} TensorParallelPair of int4-g128 d{dm}, seq {M}, "
                        f"{steps} steps, one reduction of the f32 [{M}, {dm}] partial per pair, p_sample, KV step on "
                        f"the head-sharded phase-aware cache ({heads // world} of {heads} heads per rank)",
-           "n_ranks": world}
+           "n_ranks": world, "schedule": "serial (KV step and its all-reduce in stream order, overlap=False)"}
 
     def kv_cache(cfg):
         gk = torch.Generator(device=dev).manual_seed(98)
@@ -350,10 +357,28 @@ def denoise_loop_dp(d, torch, dist, dev, world, steps):
                        f"per rank, {steps} steps, KV step on the rank's token rows (one 4-float all_reduce(MAX) per "
                        f"quantization), p_sample fused in the last layer",
            "n_ranks": world, "ms_per_step": round(s / steps * 1e3, 4), "tok_per_s_per_step": round(M / (s / steps), 1),
-           "finite": bool(torch.isfinite(out).all())}
+           "finite": bool(torch.isfinite(out).all()),
+           "schedule": "serial (KV step and its all-reduce in stream order, overlap=False); denoise_loop (1 GPU) "
+                       "overlaps the KV step on a side stream, so the two are not like-for-like"}
     for lyr in layers:
         lyr.close()
     return res
+
+
+def headline(world, M, steps, t_slice, t_full=None, chunks=1):
+    """``value`` / ``ms_per_step`` of the JSON line and where they come from.  N = 1: the GEMM step
+    (t_slice).  N > 1: the WHOLE step on every rank -- the column-slice GEMM plus the all-gather of
+    the slices into the full [M, N] Y (t_full; lib.rs:812 returns the full Y) -- with the slice GEMM
+    alone kept as the side key ``kernel_only`` (no rank holds the full Y there)."""
+    if world == 1:
+        return {"value": M * steps / t_slice, "ms_per_step": t_slice / steps * 1e3, "value_from": "gemm"}
+    if t_full is None:
+        raise ValueError("N > 1: the headline needs the gathered step's time")
+    return {"value": M * steps / t_full, "ms_per_step": t_full / steps * 1e3,
+            "value_from": f"gemm+allgather (chunks={chunks})",
+            "kernel_only": {"value": round(M * steps / t_slice, 1), "ms_per_step": round(t_slice / steps * 1e3, 5),
+                            "note": "the rank's column-slice GEMM alone (kernel only: the full Y exists on no "
+                                    "rank; not the headline)"}}
 
 
 def _timed(fn, steps, stream, torch, dist, world, dev):
@@ -448,19 +473,27 @@ def spawn_ranks(n, argv, script=None):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
         procs.append(subprocess.Popen([sys.executable, str(script or Path(__file__).resolve()), *argv], env=env))
-    rc = 0
-    try:
-        for p in procs:
-            c = p.wait()
-            if c != 0 and rc == 0:
-                rc = c
-                for q in procs:          # one rank failed: the others would hang in a collective
-                    if q.poll() is None:
-                        q.send_signal(signal.SIGTERM)
-    except KeyboardInterrupt:
+
+    def stop_all():
         for q in procs:
             if q.poll() is None:
                 q.send_signal(signal.SIGTERM)
+
+    rc = 0
+    try:
+        # Poll every child: whichever rank fails first stops the others at once (a rank blocked in
+        # a collective on a dead peer would otherwise hang until the collective's timeout).
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c is not None and c != 0]
+            if bad and rc == 0:
+                rc = bad[0]
+                stop_all()
+            if all(c is not None for c in codes):
+                break
+            time.sleep(0.05)
+    except KeyboardInterrupt:
+        stop_all()
         raise
     return rc if rc >= 0 else 128 - rc
 
@@ -525,9 +558,24 @@ def main():
         torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
-    t_max, kernel_ms = _timed(step, args.steps, stream, torch, dist, world, dev)
-    ms_per_step = t_max / args.steps * 1e3
-    value = M * args.steps / t_max
+    # the rank's slice GEMM alone: the roofline kernel (HIP events on its stream); at N = 1 this IS
+    # the step
+    t_slice, kernel_ms = _timed(step, args.steps, stream, torch, dist, world, dev)
+    t_full = None
+    if world > 1:
+        # the whole step on every rank: Y = x.dot(W) + b as the full [M, N] (lib.rs:806-813) = the
+        # rank's column-slice GEMM + the RCCL all-gather of the f16 slices into Y's rows
+        # (ColumnParallelLinear.forward_gathered; --gather-chunks > 1 overlaps chunk i's gather with
+        # chunk i+1's GEMM)
+        Yfull = torch.empty(M, N, dtype=torch.float16, device=dev)
+
+        def step_full():
+            col.forward_gathered(X, out=Yfull, stage=Y, chunks=args.gather_chunks)
+        for _ in range(max(2, args.warmup)):
+            step_full()
+        t_full, _ = _timed(step_full, args.steps, stream, torch, dist, world, dev)
+    head = headline(world, M, args.steps, t_slice, t_full, args.gather_chunks)
+    value, ms_per_step = head["value"], head["ms_per_step"]
 
     flops_local = 2.0 * M * n_local * K
     abytes_local = algorithmic_bytes(M, K, n_local, args.bits, args.group)
@@ -540,10 +588,14 @@ def main():
         "ms_per_step": round(ms_per_step, 5), "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "f16 X x exact int4 weights (f32 group scales), f32 accumulate",
         "data": "synthetic",
-        "config": {"workload": f"int{args.bits}-g{args.group} dequant+GEMM, M={M} tokens x K={K} x N={N}, "
-                               f"N split column-parallel over {world} rank(s) ({n_local} columns on rank 0)",
+        "config": {"workload": (f"int{args.bits}-g{args.group} dequant+GEMM, M={M} tokens x K={K} x N={N}" +
+                                ("" if world == 1 else
+                                 f", N split column-parallel over {world} ranks ({n_local} columns on rank 0) + "
+                                 f"RCCL all-gather of the f16 slices: the full [M, N] Y on every rank")),
                    "M": M, "K": K, "N": N, "bits": args.bits, "group": args.group,
-                   "global_batch_tokens": M, "parallelism": f"column-parallel (hidden dim) x{world}"},
+                   "global_batch_tokens": M, "parallelism": f"column-parallel (hidden dim) x{world}" +
+                                                            ("" if world == 1 else " + all-gather")},
+        "value_from": head["value_from"],
         "gib_per_s": round(algorithmic_bytes(M, K, N, args.bits, args.group) / (ms_per_step * 1e-3) / 2**30, 1),
         "tflops": round(2.0 * M * N * K / (ms_per_step * 1e-3) / 1e12, 1),
         "roofline": {"bound": "mfma", "achieved": round(achieved_tflops, 1), "peak": PEAK_F16_TFLOPS,
@@ -553,16 +605,9 @@ def main():
                      "algorithmic_bytes": abytes_local, "kernel_ms": round(kernel_ms, 5),
                      "kernel": f"rank 0's local GEMM, M={M} x K={K} x N={n_local}"},
     }
+    if "kernel_only" in head:
+        out["kernel_only"] = head["kernel_only"]
     if world > 1:
-        def step_gather():
-            lin(X, out=Y)
-            col.all_gather(Y)
-        for _ in range(2):
-            step_gather()
-        tg, _ = _timed(step_gather, args.steps, stream, torch, dist, world, dev)
-        out["with_allgather"] = {"ms_per_step": round(tg / args.steps * 1e3, 5),
-                                 "value": round(M * args.steps / tg, 1),
-                                 "note": "GEMM + RCCL all_gather of the f16 Y slices into the full [M, N] Y"}
         full = d.QuantLinear.from_weight(W, None, args.bits, args.group)
         Yf = torch.empty(M, N, dtype=torch.float16, device=dev)
         for _ in range(args.warmup):
@@ -589,8 +634,10 @@ def main():
         out["denoise_loop"] = denoise_loop(d, torch, dev)
         if world > 1 and args.tp_steps > 0:
             out["denoise_loop_tp"] = denoise_loop_tp(d, torch, dist, dev, world, args.tp_steps)
-        if world > 1:
-            out["denoise_loop_dp"] = denoise_loop_dp(d, torch, dist, dev, world, 50)
+        if world > 1 and args.dp_steps > 0:
+            if world > 2048:
+                raise SystemExit("denoise_loop_dp: the token-parallel loop needs world <= 2048 tokens")
+            out["denoise_loop_dp"] = denoise_loop_dp(d, torch, dist, dev, world, args.dp_steps)
     if args.sweep and rank == 0 and world == 1:
         out["m_sweep"] = m_sweep(lin, K, N, args.bits, args.group, torch, dev, stream)
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -628,6 +628,11 @@ extern "C" int dllm_kv_attention(const void *Q, const uint8_t *Kq, const float *
         return fail(DLLM_ERR_INVALID_PARAMS, "Q, O, K and V codes must be 16-byte aligned");   // O: 16-B row stores
     hipStream_t st = as_stream(stream);
     const int nkb = static_cast<int>((S + kKB - 1) / kKB);
+    // the attention kernel stages a head's f16 K / V images through one buffer descriptor with
+    // 32-bit offsets (blk * kImg): a head's images must stay below 2 GiB too (~560 B per key, so
+    // S past ~3.8 M keys at small H would pass the code-size check above)
+    if (static_cast<size_t>(nkb) * kImg >= (size_t{1} << 31))
+        return fail(DLLM_ERR_SHAPE_MISMATCH, "a head's K/V images must stay below 2 GiB (32-bit buffer offsets)");
     uint8_t *img = reinterpret_cast<uint8_t *>(device_workspace(st, static_cast<size_t>(H) * nkb * kImg, 8));
     if (!img) return DLLM_ERR_HIP;
     dim3 sgrid(static_cast<unsigned>(nkb), static_cast<unsigned>(H));

@@ -19,6 +19,9 @@
 #include "linear_common.hpp"
 #include "stamp.hpp"
 #include "diffusion_rng.hpp"
+#if DLLM_LAB
+#include "dllm_quant_lab.h"   // the lab build's extra entry point
+#endif
 
 #ifndef DLLM_LAB
 #define DLLM_LAB 0
@@ -999,9 +1002,11 @@ wq_decode_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__r
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (XL) {
             if (round == 0) {
-                // The block's LDS-DMAs precede this round's weight loads (at least kDepth
-                // instructions; the DMAs are older), so this count waits for the DMAs only.
-                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kDepth * (BITS == 8 ? 2 : 1)) : "memory");
+                // The block's LDS-DMAs must land before any wave reads X / scales from LDS.  The
+                // round's weight loads were issued after them, but how many VMEM instructions
+                // load_words becomes is the compiler's choice (it may split or merge them), so a
+                // count that leaves them in flight could under-wait: drain everything, once.
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
                 __builtin_amdgcn_s_barrier();
                 __builtin_amdgcn_sched_barrier(0);
             }

@@ -80,7 +80,11 @@ def token_rows(M: int, world: int, rank: int):
     """Contiguous token-row shard [r0, r1) of an M-token batch or sample (token parallelism: the
     linear layers and p_sample are per token, so rank r runs rows r0..r1 through replicated layers
     with no collective; in the denoise loop its K/V rows go to a sharded cache,
-    HeadParallelKVCacheEntry)."""
+    HeadParallelKVCacheEntry).  Every rank gets at least one row: ``world <= M`` is required (an
+    empty shard would still have to join the KV step's all_reduce, and DenoiseLoop refuses a zero-row
+    x), so a larger world raises instead of handing some ranks nothing."""
+    if not 1 <= world <= M or not 0 <= rank < world:
+        raise ValueError(f"token_rows: need 1 <= world <= M and 0 <= rank < world (M={M}, world={world}, rank={rank})")
     per, rem = divmod(M, world)
     r0 = rank * per + min(rank, rem)
     return r0, r0 + per + (1 if rank < rem else 0)
@@ -111,12 +115,70 @@ class ColumnParallelLinear:
             return y
         return self.all_gather(y)
 
-    def all_gather(self, y: torch.Tensor) -> torch.Tensor:
-        """The full [M, N] Y from every rank's column slice (one all_gather over the ranks)."""
-        parts = [torch.empty(y.shape[0], n1 - n0, dtype=y.dtype, device=y.device)
-                 for n0, n1 in (column_range(self.N, self.world, r) for r in range(self.world))]
-        dist.all_gather(parts, y.contiguous(), group=self.pg)
-        return torch.cat(parts, dim=1)
+    def _widths(self):
+        return [n1 - n0 for n0, n1 in (column_range(self.N, self.world, r) for r in range(self.world))]
+
+    def all_gather(self, y: torch.Tensor, out: Optional[torch.Tensor] = None, async_op: bool = False):
+        """The full [M, N] Y (row-major, into ``out`` when given) from every rank's column slice: ONE
+        all_gather_into_tensor of the [M, w] slices into a rank-major [world * M, w] buffer, then the
+        slices are laid side by side into Y's rows (unequal slices -- N not a multiple of 32 x world
+        -- travel padded to the widest).  ``async_op``: returns ``(finish, out)`` -- the exchange is
+        in flight on the collective's stream, and ``finish()`` makes the current stream wait for it
+        and writes ``out``."""
+        M = y.shape[0]
+        if out is None:
+            out = torch.empty(M, self.N, dtype=y.dtype, device=y.device)
+        widths = self._widths()
+        wmax = max(widths)
+        if y.shape[1] == wmax:
+            y = y.contiguous()
+        else:
+            yp = torch.zeros(M, wmax, dtype=y.dtype, device=y.device)
+            yp[:, :y.shape[1]] = y
+            y = yp
+        buf = torch.empty(self.world * M, wmax, dtype=y.dtype, device=y.device)   # rank-major slices
+        work = dist.all_gather_into_tensor(buf, y, group=self.pg, async_op=async_op)
+
+        def finish():
+            if work is not None:
+                work.wait()
+            parts = buf.view(self.world, M, wmax)
+            if len(set(widths)) == 1:
+                out.view(M, self.world, wmax).copy_(parts.transpose(0, 1))
+            else:
+                for r, (n0, n1) in enumerate(column_range(self.N, self.world, q) for q in range(self.world)):
+                    out[:, n0:n1] = parts[r, :, :n1 - n0]
+            return out
+
+        if async_op:
+            return finish, out
+        return finish()
+
+    def forward_gathered(self, x: torch.Tensor, out: Optional[torch.Tensor] = None, out_dtype=torch.float16,
+                         chunks: int = 1, stage: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """The whole layer on every rank: Y = x.dot(W) + b as the full [M, N] (lib.rs:806-813) from
+        the column shards -- each rank's slice GEMM, then the all-gather of the slices.  ``chunks`` > 1
+        splits the tokens: chunk i's all-gather (asynchronous, on the collective's stream) runs while
+        chunk i+1's GEMM computes.  Rows are independent, so every chunking gives the same Y.
+        ``stage``: an optional [M, n1 - n0] buffer for the local slices."""
+        M = x.shape[0]
+        if out is None:
+            out = torch.empty(M, self.N, dtype=out_dtype, device=x.device)
+        if stage is None:
+            stage = torch.empty(M, self.n1 - self.n0, dtype=out.dtype, device=x.device)
+        if not self.collective:
+            if self.world > 1:
+                raise ValueError("forward_gathered needs the ranks' collective (shard emulation has none)")
+            return self.local(x, out_dtype=out.dtype, out=out)
+        pending, r0 = [], 0
+        for xc in (torch.tensor_split(x, min(chunks, M), dim=0) if chunks > 1 and M > 1 else (x,)):
+            r1 = r0 + xc.shape[0]
+            yc = self.local(xc, out_dtype=out.dtype, out=stage[r0:r1])
+            pending.append(self.all_gather(yc, out=out[r0:r1], async_op=True)[0])
+            r0 = r1
+        for finish in pending:
+            finish()
+        return out
 
     __call__ = forward
 

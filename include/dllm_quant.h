@@ -15,8 +15,8 @@
  *     host pointers, stage through device memory and synchronise (parity/test convenience).
  *   - quantized codes are either one code per byte ("unpacked", the reference's storage,
  *     diffuse-llm-rs/src/quantization.rs:59-65) or the packed LSB-first bitstream below.
- *   - handles (dllm_linear_t) own device memory, are immutable after create (the lab build's
- *     dllm_linear_set_kernel_variant aside) and may be used from several threads on distinct
+ *   - handles (dllm_linear_t) own device memory, are immutable after create and may be used
+ *     from several threads on distinct
  *     streams (the reference's Send + Sync model bound).
  *
  * Packed layout (build-defined; the reference only assumes its size, quantization.rs:122):
@@ -279,13 +279,6 @@ size_t dllm_linear_weight_bytes(dllm_linear_t h);
  * parameters (f16 zero-point/scale pairs + f32 scales) -- 17.02 MiB at 4096 x 4096 int4 g128, 9.02
  * MiB prefill-only -- plus the Horner ratios where kept (+0.52 MiB there). */
 size_t dllm_linear_device_bytes(dllm_linear_t h);
-#ifdef DLLM_LAB
-/* Lab build only (libdllm_hip_lab.so): A/B schedule variants and ablation masks; mutates the
- * handle, so it is not part of the product ABI.  -1: product policy; 4: rounded-weight policy;
- * 14 / 15: exact-weight 128x256 / tile-major 256x256; 0..3, 5..13: round-1 schedules;
- * 16..23, 32..95, 100..195: ablation masks (results are garbage); 200..263: decode tile override. */
-int dllm_linear_set_kernel_variant(dllm_linear_t h, int variant);
-#endif
 int dllm_linear_destroy(dllm_linear_t h);
 
 /* ---- f3: wire formats (host buffers; no device work) --------------------------------------

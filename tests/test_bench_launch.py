@@ -7,6 +7,7 @@ import sys
 from pathlib import Path
 
 import bench
+import pytest
 
 ROOT = Path(__file__).resolve().parents[1]
 
@@ -52,3 +53,29 @@ def test_spawn_ranks_reports_failure(tmp_path):
     probe = tmp_path / "fail.py"
     probe.write_text("import os, sys\nsys.exit(3 if os.environ['RANK'] == '1' else 0)\n")
     assert bench.spawn_ranks(2, [], script=probe) == 3
+
+
+def test_spawn_ranks_stops_blocked_rank0_when_rank1_fails(tmp_path):
+    """Rank 0 blocked (as in a collective on a dead peer) while rank 1 exits 3: spawn_ranks returns
+    3 promptly and stops rank 0, instead of waiting on rank 0 first."""
+    probe = tmp_path / "hang.py"
+    probe.write_text("import os, sys, time\n"
+                     "if os.environ['RANK'] == '1':\n"
+                     "    sys.exit(3)\n"
+                     "time.sleep(600)\n")
+    t0 = __import__("time").perf_counter()
+    assert bench.spawn_ranks(2, [], script=probe) == 3
+    assert __import__("time").perf_counter() - t0 < 30
+
+
+def test_headline_value_is_the_whole_step_at_n_gt_1():
+    """N > 1: ``value`` comes from the gathered step (slice GEMM + all-gather, the full Y on every
+    rank), never from the slice GEMM alone, which stays the side key ``kernel_only``."""
+    h1 = bench.headline(1, 4096, 10, t_slice=1e-3)
+    assert h1["value_from"] == "gemm" and h1["value"] == 4096 * 10 / 1e-3 and "kernel_only" not in h1
+    h4 = bench.headline(4, 4096, 10, t_slice=0.4e-3, t_full=0.9e-3, chunks=2)
+    assert h4["value"] == 4096 * 10 / 0.9e-3 and abs(h4["ms_per_step"] - 0.09) < 1e-12
+    assert h4["value_from"].startswith("gemm+allgather")
+    assert h4["kernel_only"]["value"] == round(4096 * 10 / 0.4e-3, 1)
+    with pytest.raises(ValueError):
+        bench.headline(2, 4096, 10, t_slice=1e-3)

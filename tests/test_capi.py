@@ -9,13 +9,21 @@ import pytest
 
 ROOT = Path(__file__).resolve().parents[1]
 HEADER = ROOT / "include" / "dllm_quant.h"
+LAB_HEADER = ROOT / "include" / "dllm_quant_lab.h"   # the lab build's extra entry points only
 
 
 def declared_symbols(lab=False):
-    text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
-    if not lab:   # the lab build's entry points are not part of the product ABI
-        text = re.sub(r"#ifdef DLLM_LAB.*?#endif", "", text, flags=re.S)
+    """Symbols of the product header; ``lab``: plus those of the lab-only header."""
+    text = "".join(re.sub(r"/\*.*?\*/", "", h.read_text(), flags=re.S)
+                   for h in ((HEADER, LAB_HEADER) if lab else (HEADER,)))
     return sorted(set(re.findall(r"\b(dllm_\w+)\s*\(", text)))
+
+
+def test_product_header_declares_no_lab_entry_point():
+    """The product header is the product ABI only: no lab section, no lab entry point."""
+    text = HEADER.read_text()
+    assert "DLLM_LAB" not in text and "set_kernel_variant" not in text
+    assert declared_symbols(lab=True) != declared_symbols()
 
 
 def test_header_symbols_exported(dllm):

@@ -76,6 +76,13 @@ def _worker(rank, world, port, outdir):
     col = par.ColumnParallelLinear(WA, bA, 4, 128, gather=True, local_factory=OracleLinear)
     res["col_y"] = col(X, out_dtype=torch.float32).numpy()
     res["col_codes"], res["col_range"] = col.local.codes, np.array([col.n0, col.n1])
+    # the whole layer on every rank (bench.py's N > 1 value): slice GEMMs + all-gather, unchunked and
+    # with the gather of chunk i overlapping chunk i+1's GEMM; and unequal slices (the list gather)
+    res["col_gathered"] = col.forward_gathered(X, out_dtype=torch.float32).numpy()
+    res["col_gathered_chunked"] = col.forward_gathered(X, out_dtype=torch.float32, chunks=5).numpy()
+    col_odd = par.ColumnParallelLinear(WB[:, :352], bB[:352], 4, 128, local_factory=OracleLinear)
+    res["col_odd_widths"] = np.array(col_odd._widths())
+    res["col_odd_gathered"] = col_odd.forward_gathered(X @ WA, out_dtype=torch.float32, chunks=2).numpy()
     row = par.RowParallelLinear(WA, bA, 4, 128, local_factory=OracleLinear)
     res["row_y"] = row(X, out_dtype=torch.float32).numpy()
     res["row_scales"], res["row_range"] = row.local.scales, np.array([row.k0, row.k1])
@@ -124,6 +131,22 @@ def test_shard_quantization_is_bitexact(gloo_results, orc):
         assert np.array_equal(r["col_codes"], codes[:, n0:n1])
         k0, k1 = r["row_range"]
         assert np.array_equal(r["row_scales"], scales[k0 // 128:k1 // 128])
+
+
+def test_column_gathered_is_the_whole_layer(gloo_results):
+    """forward_gathered (bench.py's N > 1 step) leaves the full [M, N] Y on every rank, equal to the
+    unsharded layer, for any token chunking and for unequal column slices."""
+    WA, WB, bA, bB, X = _reference()
+    Y = OracleLinear(torch.from_numpy(WA), torch.from_numpy(bA), 4, 128)(torch.from_numpy(X)).numpy()
+    H = (torch.from_numpy(X) @ torch.from_numpy(WA)).numpy()
+    Yb = OracleLinear(torch.from_numpy(WB[:, :352]), torch.from_numpy(bB[:352]), 4, 128)(torch.from_numpy(H)).numpy()
+    for r in gloo_results:
+        assert r["col_gathered"].shape == Y.shape
+        np.testing.assert_allclose(r["col_gathered"], Y, rtol=0, atol=1e-6)
+        assert np.array_equal(r["col_gathered_chunked"], r["col_gathered"])
+        assert len(set(r["col_odd_widths"].tolist())) == 2          # the list-gather path ran
+        np.testing.assert_allclose(r["col_odd_gathered"], Yb, rtol=0, atol=1e-5)
+    assert np.array_equal(gloo_results[0]["col_gathered"], gloo_results[1]["col_gathered"])
 
 
 def test_parallel_outputs_match_unsharded(gloo_results, orc):

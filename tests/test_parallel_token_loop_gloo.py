@@ -87,6 +87,18 @@ def test_token_rows_partition():
         assert rows[0][0] == 0 and rows[-1][1] == M
         assert all(a[1] == b[0] for a, b in zip(rows, rows[1:]))
         assert max(b - a for a, b in rows) - min(b - a for a, b in rows) <= 1
+        assert min(b - a for a, b in rows) >= 1
+
+
+def test_token_rows_refuses_empty_shards():
+    """world > M would hand some ranks zero rows (which could not join the KV step's collective):
+    refused, as are ranks outside the world."""
+    import __graft_entry__ as g
+    par = g.load_package().parallel
+    for M, W, r in ((3, 4, 0), (0, 1, 0), (8, 2, 2), (8, 2, -1), (8, 0, 0)):
+        with pytest.raises(ValueError):
+            par.token_rows(M, W, r)
+    assert par.token_rows(4, 4, 3) == (3, 4)
 
 
 def test_token_parallel_steps_bitexact(results, unsharded):
