@@ -1403,6 +1403,52 @@ bool horner_kg2_ready(const dllm_linear *hc, int M) {
     return t256 < kCUs && t128 < kCUs && tk >= kCUs;
 }
 
+// The producer / consumer Horner kernel (128 x 256 tiles, linear_pc.hip): where the 256 x 256
+// Horner grid does not fill a round and the 128 x 256 grid does (N = 4096: M 1921..4096 minus the
+// Horner grid's own range; M = 2048 = config C2 and the C5 layers; the 2-GPU column shard).
+#ifndef DLLM_HORNER_PC
+#define DLLM_HORNER_PC 1
+#endif
+bool horner_pc_ready(const dllm_linear *hc, int M, hipStream_t st) {
+#if DLLM_HORNER_PC
+    const int np = static_cast<int>(hc->Npad);
+    if (!horner_shape(hc) || hc->hstate != 1) return false;
+#if DLLM_LAB
+    if (hc->variant == 14 || hc->variant == 28) return false;   // lab A/B: the fold-form exact policy
+#endif
+    const int t128 = ((M + 127) / 128) * (np / 256);
+    return t128 >= kCUs && !horner_ready(hc, M, st);
+#else
+    (void)hc; (void)M; (void)st;
+    return false;
+#endif
+}
+
+// The two-k-group PC kernel (128 x 128 tiles, linear_pc.hip): where none of the larger Horner grids
+// fills a round and 128 x 128 tiles fill exactly one (the 4-GPU column shard M = 4096 x N 1024;
+// M = 2048 x N 2048; M = 1024 x N 4096).
+#ifndef DLLM_HORNER_PC_KG2
+#define DLLM_HORNER_PC_KG2 1
+#endif
+bool horner_kg2_ready(const dllm_linear *hc, int M);
+bool horner_pc_kg2_ready(const dllm_linear *hc, int M, hipStream_t st) {
+#if DLLM_HORNER_PC_KG2
+    const int np = static_cast<int>(hc->Npad);
+    if (!(hc->precision == DLLM_PRECISION_EXACT && hc->bits == 4 && hc->group == 128 && hc->K % 256 == 0 &&
+          np % 128 == 0 && hc->hstate == 1))
+        return false;
+#if DLLM_LAB
+    if (hc->variant == 14 || hc->variant == 28) return false;   // lab A/B: the fold-form exact policy
+#endif
+    const int t128 = ((M + 127) / 128) * (np / 128);
+    return t128 >= kCUs && t128 < 2 * kCUs && !horner_ready(hc, M, st) && !horner_pc_ready(hc, M, st) &&
+           !horner_kg2_ready(hc, M);
+#else
+    (void)hc; (void)M; (void)st;
+    return false;
+#endif
+}
+
 template <typename YT, int EPI>
 int launch_horner(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t st, const PSampleEpi *epi) {
 #if DLLM_LAB
@@ -1463,10 +1509,20 @@ int launch_prefill_auto(const dllm_linear *h, const __half *X, int M, YT *Y, hip
 #endif
     if (use_exact(h)) {
         if (BITS == 4 && horner_ready(h, M, st)) return launch_horner<YT, EPI>(h, X, M, Y, st, epi);
+        if (BITS == 4 && horner_pc_ready(h, M, st)) {
+            const HornerGemmArgs a{X, M, (int)h->K, h->wdev, h->sz, h->hr, h->sf, h->bias, Y, (int)h->N,
+                                   (int)h->Npad, epi};
+            return launch_horner_pc_gemm(a, std::is_same<YT, float>::value ? 1 : 0, st);
+        }
         if (BITS == 4 && horner_kg2_ready(h, M)) {
             const HornerGemmArgs a{X, M, (int)h->K, h->wdev, h->sz, h->hr, h->sf, h->bias, Y, (int)h->N,
                                    (int)h->Npad, epi};
             return launch_horner_kg2_gemm(a, std::is_same<YT, float>::value ? 1 : 0, st);
+        }
+        if (BITS == 4 && horner_pc_kg2_ready(h, M, st)) {
+            const HornerGemmArgs a{X, M, (int)h->K, h->wdev, h->sz, h->hr, h->sf, h->bias, Y, (int)h->N,
+                                   (int)h->Npad, epi};
+            return launch_horner_pc_kg2_gemm(a, std::is_same<YT, float>::value ? 1 : 0, st);
         }
 #if DLLM_LAB
         if (const int rows = BITS == 4 ? horner_rows(h, M) : 0) {   // lab A/B 323 only

@@ -851,9 +851,13 @@ __global__ void __launch_bounds__(kBlock) adaptive_quantize_kernel(const float *
 
 inline bool aligned(const void *p, size_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; }
 
-inline unsigned octet_grid(size_t n) { return grid_for((n + 7) / 8, kBlock, kCUs * 16); }
+#ifndef DLLM_GRID_CAP   // A/B builds: every streaming quantization kernel on at most this many blocks
+#define DLLM_GRID_CAP 0
+#endif
+constexpr unsigned kCapOr(unsigned c) { return DLLM_GRID_CAP ? DLLM_GRID_CAP : c; }
+inline unsigned octet_grid(size_t n) { return grid_for((n + 7) / 8, kBlock, kCapOr(kCUs * 16)); }
 
-constexpr unsigned kMinmaxBlocks = 1024;
+constexpr unsigned kMinmaxBlocks = kCapOr(1024);
 
 inline int launch_minmax(const float *x, size_t n, float2 *partials, unsigned nblk, hipStream_t st) {
     size_t head = 0;
@@ -885,7 +889,7 @@ inline bool fused_width(int b) { return b == 1 || b == 2 || b == 4 || b == 8; }
 
 // Grid of quantize_fused_kernel: two full octets per thread per trip, at most 8 blocks per CU
 // (all resident, so the prologue's 8 KiB partials read overlaps other blocks' streaming).
-inline unsigned fused_grid(size_t n) { return grid_for((n / 8 + 1) / 2, kBlock, kCUs * 8); }
+inline unsigned fused_grid(size_t n) { return grid_for((n / 8 + 1) / 2, kBlock, kCapOr(kCUs * 8)); }
 
 template <int BA>
 int launch_fused_b(const float *x, size_t n, const float2 *partials, int np, uint8_t *out_a, float *params_a, int bb,

@@ -21,6 +21,11 @@ for sh in %r.split(","):
     Y = torch.empty(M, N, dtype=torch.float16, device="cuda")
     for _ in range(30): lin(X, out=Y)
     torch.cuda.synchronize()
+    import time as _t
+    t0 = _t.perf_counter()
+    while _t.perf_counter() - t0 < %r:   # PREWARM_MS: the clocks' steady state before timing
+        for _ in range(20): lin(X, out=Y)
+        torch.cuda.synchronize()
     ts = []
     for r in range(5):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -39,7 +44,7 @@ shapes = os.environ.get("SHAPES", "4096:4096,2048:4096,4096:1024,4096:512")
 for rnd in range(int(os.environ.get("ROUNDS", "3"))):
     for lib in libs:
         env = dict(os.environ, DLLM_LIB=str((ROOT / lib).resolve()))
-        res = subprocess.run([sys.executable, "-c", CODE % (str(ROOT), shapes)], env=env, capture_output=True, text=True,
+        res = subprocess.run([sys.executable, "-c", CODE % (str(ROOT), shapes, float(os.environ.get("PREWARM_MS", "0")) / 1e3)], env=env, capture_output=True, text=True,
                              timeout=300)
         line = [l for l in res.stdout.splitlines() if l.startswith("{")]
         print(json.dumps({"lib": lib, "round": rnd, **(json.loads(line[-1]) if line else {"error": res.stderr[-400:]})}),

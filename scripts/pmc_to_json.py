@@ -17,12 +17,14 @@ for f in glob.glob(f"{root}/**/pmc_counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         if regex in r["Kernel_Name"]:
             vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
-fetch = statistics.median(vals["FETCH_SIZE"]) * 1024
-write = statistics.median(vals["WRITE_SIZE"]) * 1024
-res = {"kernel": regex, "FETCH_SIZE_bytes_raw": fetch, "WRITE_SIZE_bytes": write,
-       "hbm_bytes_per_launch": 2 * fetch + write,
-       "correction": "FETCH_SIZE doubled (gfx950 reports 1/2 of wide coalesced reads); Infinity-Cache hits are counted",
-       "dispatches": len(vals["FETCH_SIZE"])}
+res = {"kernel": regex}
+if "FETCH_SIZE" in vals and "WRITE_SIZE" in vals:   # SQ-only records carry no HBM figure
+    fetch = statistics.median(vals["FETCH_SIZE"]) * 1024
+    write = statistics.median(vals["WRITE_SIZE"]) * 1024
+    res.update({"FETCH_SIZE_bytes_raw": fetch, "WRITE_SIZE_bytes": write, "hbm_bytes_per_launch": 2 * fetch + write,
+                "correction": "FETCH_SIZE doubled (gfx950 reports 1/2 of wide coalesced reads); Infinity-Cache hits "
+                              "are counted",
+                "dispatches": len(vals["FETCH_SIZE"])})
 if cfg is not None:
     res["config"] = cfg
 for k, v in vals.items():

@@ -452,8 +452,9 @@ def test_linear_split_k_exact_integers(dllm, torch, orc):
 def test_linear_policy_exact_integers(dllm, torch, orc, precision, bits, M, N):
     """Every tile of both precision policies on exact-integer data (each group spans [0, 2^b - 1]:
     scale 1, zp 0; K = 768 = 6 groups, so every product and partial sum is an exact integer):
-    exact weights -- the Horner kernel (int4, M 4096 at N 4096), the 128 x 256 fold-form tiles (M 2048),
-    the KG2 Horner tiles (int4, M 1800),
+    exact weights -- the Horner kernel (int4, M 4096 at N 4096), the producer/consumer 128 x 256
+    tiles (int4, M 2048; other widths: the 128 x 256 fold-form tiles), the KG2 Horner tiles (int4,
+    M 1800), the two-k-group producer/consumer 128 x 128 tiles (int4, N 1024 at M 4096),
     128 x 128 + group-aligned split-K
     (N 1024 / 512, M 512, 300), the exact decode kernel (M <= 64, one or 4 column tiles, K split) --
     and rounded weights (256 x 256, 256 x 128 two k-groups, 128 x 128 split-K, decode), with bias,
@@ -503,11 +504,13 @@ def test_linear_exact_weights_tight(dllm, torch, orc, M, N, group):
 
 @pytest.mark.parametrize("spread,M,K", [(8, 4096, 4096), (8, 8000, 1024), (8, 4300, 1024), (30, 4096, 2048), (45, 4096, 1024),
                                          (8, 1800, 4096), (30, 1850, 2048), (45, 1800, 1024),
-                                         (8, 2048, 4096), (30, 3000, 2048), (45, 2048, 1024)])
+                                         (8, 2048, 4096), (30, 3000, 2048), (45, 2048, 1024),
+                                         (8, 1024, 4096), (30, 1000, 2048), (45, 1024, 1024)])
 def test_linear_horner_scale_spread(dllm, torch, orc, spread, M, K):
     """The 256 x 256-tile exact kernel (int4 g128, >= 256 tiles) keeps one accumulator in Horner form:
-    acc <- acc * (s_{g-1} / s_g) + T_g, times s_{G-1} at the end; at M = 2048 / 3000 the fold form
-    runs (the 256 x 256 grid leaves CUs idle); at M = 1800 / 1850 (120 such tiles,
+    acc <- acc * (s_{g-1} / s_g) + T_g, times s_{G-1} at the end; at M = 2048 / 3000 the same form
+    runs on the producer/consumer 128 x 256 tiles, at M = 1024 / 1000 on the two-k-group 128 x 128
+    producer/consumer tiles (one chain per K-half); at M = 1800 / 1850 (120 such tiles,
     240 of the fold form's 128 x 256) the 256 x 128-tile KG2 kernel runs one chain per K-half (the
     second starting from a zero accumulator) and sums the two halves' partials times their last
     scales.  Per-(group, column) weight
@@ -902,12 +905,13 @@ def test_gemm_variants_bit_identical(dllm, torch):
 
 @pytest.mark.parametrize("K", [128, 256, 384, 1152])
 def test_linear_staggered_tiles_exact_integers(dllm, torch, K):
-    """The 128 x 256 exact fold tiles with staggered wave halves (linear_exact.hip, DLLM_EXACT_STAG:
-    a 4-slot ring, stage kt + 2 issued in step kt, the late half's share of stage kt + 1 awaited at
-    the mid-step barrier), product policy, on exact-integer data: every partial is exact, so each
-    output equals the f64 product bit for bit.  M 2048 / 2100 x N 4096 take those tiles (>= 256 of
-    them; 2100 leaves a ragged last row block); K 128 / 256 / 384 run fewer stages than the ring
-    keeps in flight (1 / 2 / 3), K 1152 a ring period that does not divide the stage count."""
+    """The 128 x 256 exact tiles, product policy, on exact-integer data: every partial is exact, so
+    each output equals the f64 product bit for bit.  int4 g128 with valid Horner ratios runs the
+    producer/consumer kernel (linear_pc.hip: 8 consumer waves, 4 producer waves issuing every DMA
+    piece, consumer halves half a stage apart, one 12-wave barrier per half stage, 3-slot ring).
+    M 2048 / 2100 x N 4096 take those tiles (>= 256 of them; 2100 leaves a ragged last row block);
+    K 128 / 256 / 384 run fewer stages than the ring keeps in flight (1 / 2 / 3), K 1152 a ring
+    period that does not divide the stage count."""
     N = 4096
     rng = np.random.default_rng(K)
     W = rng.integers(0, 16, (K, N)).astype(np.float32)
@@ -922,6 +926,29 @@ def test_linear_staggered_tiles_exact_integers(dllm, torch, K):
         assert np.array_equal(host(lin(Xd, out_dtype=torch.float32)), ref), (K, M)
         Y16 = host(lin(Xd, out_dtype=torch.float16).float())
         assert np.array_equal(Y16, ref.astype(np.float16).astype(np.float32)), (K, M, "f16")
+    lin.close()
+
+
+@pytest.mark.parametrize("K", [256, 512, 768, 2304])
+@pytest.mark.parametrize("M,N", [(4096, 1024), (2048, 2048), (1024, 4096), (1000, 4096), (4096, 1020)])
+def test_linear_pc_kg2_tiles_exact_integers(dllm, torch, K, M, N):
+    """The two-k-group producer/consumer kernel (linear_pc.hip, 128 x 128 tiles: the 4-GPU column
+    shard 4096 x 1024, 2048 x 2048, 1024 x 4096) on exact-integer data, bit-equal to the f64 product
+    for f32 and f16 outputs: K-half kg's Horner chain in k-group kg, the halves' partials summed in
+    a fixed order.  K 256 .. 2304 = 1 .. 9 groups per half (a ring period of 3 stages that does not
+    divide the 2 .. 18 k-steps of a half); M 1000 leaves a ragged last row block, N 1020 a padded
+    last column block (the 8-B row-store path)."""
+    rng = np.random.default_rng(K + M + N)
+    W = rng.integers(0, 16, (K, N)).astype(np.float32)
+    for g0 in range(0, K, 128):
+        W[g0, :], W[g0 + 1, :] = 0.0, 15.0
+    b = rng.integers(-4, 5, N).astype(np.float32)
+    X = rng.integers(-2, 3, (M, K)).astype(np.float32)
+    lin = dllm.QuantLinear.from_weight(dev(torch, W), dev(torch, b), 4, 128, prefill_only=True)
+    ref = (X.astype(np.float64) @ W.astype(np.float64) + b).astype(np.float32)
+    Xd = dev(torch, X).half()
+    assert np.array_equal(host(lin(Xd, out_dtype=torch.float32)), ref), (K, M, N)
+    assert np.array_equal(host(lin(Xd, out_dtype=torch.float16).float()), ref.astype(np.float16).astype(np.float32))
     lin.close()
 
 
