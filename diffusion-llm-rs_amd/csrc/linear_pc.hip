@@ -46,6 +46,9 @@
 #ifndef DLLM_PC_STAG
 #define DLLM_PC_STAG 1
 #endif
+#ifndef DLLM_PC_KG2_STAG   // the same stagger in the two-k-group kernel (k-group 1 behind k-group 0)
+#define DLLM_PC_KG2_STAG DLLM_PC_STAG
+#endif
 // DLLM_PC_MF: the consumers' MFMA shape.  16: 16x16x32 (wq_horner16_kernel's fragments; per wave 2
 // column blocks x 8 token blocks); 32: 32x32x16 (per wave 4 token reps of 32 x 32, A fragments
 // straight from the prefill layout's words -- no permlane swap -- and half the MFMA issue per flop).
@@ -797,7 +800,7 @@ wq_horner_pc_kg2_kernel(const __half *__restrict__ X, int M, int K, const uint32
         }
         __builtin_amdgcn_s_barrier();
         int slot = 2;
-#if DLLM_PC_STAG
+#if DLLM_PC_KG2_STAG
         for (int u = 0; u < nk2; ++u) {
             __builtin_amdgcn_s_barrier();
             if (u + 2 < nk2) {
@@ -944,7 +947,7 @@ wq_horner_pc_kg2_kernel(const __half *__restrict__ X, int M, int K, const uint32
         make_a(0, a00, a01);
         half_step(sx, bP, bQ, 0, 0, GF);
         half_step(sx, bQ, bP, 0, 1, GF);
-#if DLLM_PC_STAG
+#if DLLM_PC_KG2_STAG
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
 #endif
@@ -958,7 +961,7 @@ wq_horner_pc_kg2_kernel(const __half *__restrict__ X, int M, int K, const uint32
     using GFf = std::integral_constant<bool, false>;
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-#if DLLM_PC_STAG
+#if DLLM_PC_KG2_STAG
     const bool late = kg == 1;
     if (late) __builtin_amdgcn_s_barrier();
 #endif
@@ -975,7 +978,7 @@ wq_horner_pc_kg2_kernel(const __half *__restrict__ X, int M, int K, const uint32
             step(2, GFf{});
         }
     }
-#if DLLM_PC_STAG
+#if DLLM_PC_KG2_STAG
     if (!late) __builtin_amdgcn_s_barrier();
 #endif
     // this half's partial: acc times the half's last group scales
