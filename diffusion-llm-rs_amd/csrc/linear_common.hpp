@@ -359,8 +359,9 @@ int launch_horner_kg2_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st);
 // The same Horner form on 128 x 256 tiles with producer / consumer waves (linear_pc.hip): 8 waves
 // compute, 4 issue every LDS-DMA of the stage ring.  Needs K % 128 == 0 and Npad % 256 == 0.
 int launch_horner_pc_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st);
-// Its two-k-group form on 128 x 128 tiles (linear_pc.hip): needs K % 256 == 0 and Npad % 128 == 0.
-int launch_horner_pc_kg2_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st);
+// Its two-k-group form on rows x 128 tiles, rows = 128 / 64 / 32 (linear_pc.hip): needs K % 256 == 0
+// and Npad % 128 == 0.
+int launch_horner_pc_kg2_gemm(const HornerGemmArgs &a, int rows, int y_f32, hipStream_t st);
 bool exact_gemm_supported(int M, int K, int Npad, int group);
 
 // Ping-pong 256 x 256 GEMM (linear_pp.hip): Y = X . W^ + b for the 256-column-tile grid, bits in

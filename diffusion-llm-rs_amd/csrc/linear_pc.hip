@@ -647,15 +647,39 @@ wq_horner_pc_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *
         }
     }
     if constexpr (EPI == 1) {
+        // token block t + 1's x_t values and row coefficients are loaded before block t's stores
+        // (psample4_x): each block's loads are in flight during the previous block's noise draw,
+        // instead of one serial round trip per 4-column group behind the stores
+        float4 xa[2], xn[2];
+        float ca[3], cn[3];
+        auto load_blk = [&](int t, float4 (&x)[2], float (&c)[3]) __attribute__((always_inline)) {
+            const int m = m0 + 16 * t + row16;
+            const bool mok = m < M;
+            const float *cp = epi.coef + 3 * ((mok ? m : 0) / epi.rps);
+            c[0] = cp[0]; c[1] = cp[1]; c[2] = cp[2];
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb)
+                x[cb] = mok && nc0 + 16 * cb < N
+                            ? *reinterpret_cast<const float4 *>(epi.x_t + static_cast<size_t>(m) * N + nc0 + 16 * cb)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+        };
+        load_blk(0, xa, ca);
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
+            if (t + 1 < 8) load_blk(t + 1, xn, cn);
             const int m = m0 + 16 * t + row16;
-            if (m >= M) continue;
+            if (m < M) {
 #pragma unroll
-            for (int cb = 0; cb < 2; ++cb) {
-                if (nc0 + 16 * cb >= N) continue;
-                psample4(epi, m, nc0 + 16 * cb, N, acc[t][cb][0] + bv[cb].x, acc[t][cb][1] + bv[cb].y,
-                         acc[t][cb][2] + bv[cb].z, acc[t][cb][3] + bv[cb].w);
+                for (int cb = 0; cb < 2; ++cb) {
+                    if (nc0 + 16 * cb >= N) continue;
+                    psample4_x(epi, static_cast<size_t>(m) * N + nc0 + 16 * cb, xa[cb], ca[0], ca[1], ca[2],
+                               acc[t][cb][0] + bv[cb].x, acc[t][cb][1] + bv[cb].y, acc[t][cb][2] + bv[cb].z,
+                               acc[t][cb][3] + bv[cb].w);
+                }
+            }
+            if (t + 1 < 8) {
+                xa[0] = xn[0]; xa[1] = xn[1];
+                ca[0] = cn[0]; ca[1] = cn[1]; ca[2] = cn[2];
             }
         }
         return;
@@ -716,19 +740,31 @@ wq_horner_pc_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *
 // lanes 32..63 repeating 0..31); 3 stages in a ring (132 KiB).  Producers: per stage 8 X pieces,
 // 2 weight pieces and (group-first stages) 1 group piece each.  STAG (as DLLM_PC_STAG): k-group 1
 // (waves 4..7, each SIMD's second consumer) runs half a stage behind k-group 0.
-constexpr int kK2XB = 2 * kPcXSub;                 // X of both halves per stage (32 KiB)
-constexpr int kK2W = 8 * 1024;                     // 2 halves x 4 column waves x 1 KiB
-constexpr int kK2G = 4 * 1024;                     // 2 halves x (sz, ratios) x 1 KiB
-constexpr int kK2Stage = kK2XB + kK2W + kK2G;      // 45056 B; 3 stages = 132 KiB
-constexpr int kK2Pieces = 8 + 2;                   // per producer per stage, + 1 on group-first stages
+// TB = token blocks of 16 per tile: 8 (128 x 128 tiles), 4 (64 x 128: M = 512 at N = 4096, the
+// 8-GPU shard 4096 x 512) or 2 (32 x 128: M = 256).
+template <int TB>
+struct K2L {
+    static_assert(TB == 8 || TB == 4 || TB == 2, "128-, 64- or 32-token tiles");
+    static constexpr int kRows = 16 * TB;
+    static constexpr int kXSub = kRows * kBK * 2;          // one half's 64-deep X sub-tile
+    static constexpr int kXB = 2 * kXSub;                   // X of both halves per stage
+    static constexpr int kW = 8 * 1024;                     // 2 halves x 4 column waves x 1 KiB
+    static constexpr int kG = 4 * 1024;                     // 2 halves x (sz, ratios) x 1 KiB
+    static constexpr int kStage = kXB + kW + kG;            // TB 8: 45056 B (3 stages = 132 KiB)
+    static constexpr int kXP = TB / 2;                      // X row blocks per producer per half
+    static constexpr int kPieces = 2 * kXP + 2;             // per producer per stage, + 1 on group-first stages
+    static constexpr int kXch = TB * 8 * 1024;              // k-group 1's hand-off area, then the f16 image
+    static_assert(kXch + kRows * 256 <= kPcRing * kStage, "epilogue fits the drained ring");
+};
 
-template <typename YT, int EPI>
+template <typename YT, int EPI, int TB>
 __global__ void __launch_bounds__(kPcThreads, 1)
 wq_horner_pc_kg2_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdev,
                         const uint32_t *__restrict__ sz, const float *__restrict__ hr, const float *__restrict__ sf,
                         const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad, int nbm, int nbn,
                         PSampleEpi epi) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kPcRing * kK2Stage];
+    using L = K2L<TB>;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kPcRing * L::kStage];
 
     // XCD-aware remap; tiles in groups of 4 row blocks, column-major inside a group (an XCD's 32
     // concurrent tiles: 4 row blocks x 8 column blocks)
@@ -742,21 +778,21 @@ wq_horner_pc_kg2_kernel(const __half *__restrict__ X, int M, int K, const uint32
 
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int m0 = bm * kPcRows, n0 = bn * 128;
+    const int m0 = bm * L::kRows, n0 = bn * 128;
     const int nk = K / kBK, nk2 = nk / 2;   // k-steps; k-steps per K-half = stages (even: K % 256 == 0)
     const uint32_t sbase = __builtin_amdgcn_readfirstlane(lds_addr(smem));
-    const bool full = (m0 + kPcRows <= M) && (n0 + 128 <= N) && (N % 8) == 0;
+    const bool full = (m0 + L::kRows <= M) && (n0 + 128 <= N) && (N % 8) == 0;
     constexpr bool kHalfY = std::is_same<YT, __half>::value && EPI == 0;
     float4 *part = reinterpret_cast<float4 *>(smem);   // k-group 1's sums (64 KiB), then the f16 image
-    uint8_t *img = smem + 64 * 1024;
+    uint8_t *img = smem + L::kXch;
 
     if (wave >= kPcCons) {
         // ---------------- producer p: X row blocks p + 4 j of both halves; the words of half p >> 1,
         // column waves 2 (p & 1) and 2 (p & 1) + 1; group data: half p >> 1, sz (p even) / ratios
         const int p = wave - kPcCons;
-        uint32_t xo[4];
+        uint32_t xo[L::kXP];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < L::kXP; ++j) {
             const int row = (p + 4 * j) * 8 + (lane >> 3);
             const int rrow = (m0 + row < M ? m0 + row : M - 1) - m0;
             const int c = (lane & 7) ^ ((row >> 1) & 5);
@@ -771,25 +807,25 @@ wq_horner_pc_kg2_kernel(const __half *__restrict__ X, int M, int K, const uint32
             raw_rsrc((p & 1) == 0 ? static_cast<const void *>(sz + n0) : static_cast<const void *>(hr + n0));
         const uint32_t vo = static_cast<uint32_t>(lane * 16), go = static_cast<uint32_t>((lane & 31) * 16);
         auto stage = [&](int slot, int kt) __attribute__((always_inline)) {
-            const uint32_t base = sbase + static_cast<uint32_t>(slot * kK2Stage);
+            const uint32_t base = sbase + static_cast<uint32_t>(slot * L::kStage);
 #pragma unroll
             for (int kg = 0; kg < 2; ++kg) {
                 const uint32_t sx = static_cast<uint32_t>((kg * nk2 + kt) * kBK * 2);
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    blds16_asm(xr, xo[j], sx, base + static_cast<uint32_t>(kg * kPcXSub + (p + 4 * j) * 1024));
+                for (int j = 0; j < L::kXP; ++j)
+                    blds16_asm(xr, xo[j], sx, base + static_cast<uint32_t>(kg * L::kXSub + (p + 4 * j) * 1024));
             }
             const uint32_t sw = static_cast<uint32_t>((wkg * nk2 + kt) * 1024);
-            blds16_asm(wr0, vo, sw, base + static_cast<uint32_t>(kK2XB + wkg * 4096 + nwa * 1024));
-            blds16_asm(wr1, vo, sw, base + static_cast<uint32_t>(kK2XB + wkg * 4096 + (nwa + 1) * 1024));
+            blds16_asm(wr0, vo, sw, base + static_cast<uint32_t>(L::kXB + wkg * 4096 + nwa * 1024));
+            blds16_asm(wr1, vo, sw, base + static_cast<uint32_t>(L::kXB + wkg * 4096 + (nwa + 1) * 1024));
             if ((kt & 1) == 0)   // a group's first k-step: this half's sz pairs or ratios
                 blds16_asm(gr, go, static_cast<uint32_t>(((wkg * nk2 + kt) >> 1) * Npad * 4),
-                           base + static_cast<uint32_t>(kK2XB + kK2W + wkg * 2048 + (p & 1) * 1024));
+                           base + static_cast<uint32_t>(L::kXB + L::kW + wkg * 2048 + (p & 1) * 1024));
         };
         // until only the newest stage (k-step kt2) is in flight
         auto wait_one = [&](int kt2) __attribute__((always_inline)) {
-            if ((kt2 & 1) == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kK2Pieces + 1) : "memory");
-            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kK2Pieces) : "memory");
+            if ((kt2 & 1) == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L::kPieces + 1) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L::kPieces) : "memory");
         };
         stage(0, 0);
         if (nk2 > 1) {
@@ -829,7 +865,7 @@ wq_horner_pc_kg2_kernel(const __half *__restrict__ X, int M, int K, const uint32
         if (!(kHalfY && full)) return;
         __syncthreads();   // the f16 image
         const int c = lane & 15;
-        for (int i = wave; i < kPcRows / 4; i += kPcCons + kPcProd) {
+        for (int i = wave; i < L::kRows / 4; i += kPcCons + kPcProd) {
             const int t = 4 * i + (lane >> 4);
             const uint4 v = *reinterpret_cast<const uint4 *>(img + t * 256 + ((c ^ (t & 15)) * 16));
             typedef unsigned int u4nt __attribute__((ext_vector_type(4)));
@@ -841,9 +877,10 @@ wq_horner_pc_kg2_kernel(const __half *__restrict__ X, int M, int K, const uint32
 
     // ---------------- consumer (kg, nw): columns n0 + 32 nw .. + 32, 128 tokens, K-half kg
     const int kg = wave >> 2, nw = wave & 3;
-    fx4p_t acc[8][2];
+    constexpr int kHB = TB / 2;   // token blocks per half step
+    fx4p_t acc[TB][2];
 #pragma unroll
-    for (int t = 0; t < 8; ++t)
+    for (int t = 0; t < TB; ++t)
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) acc[t][cb] = fx4p_t{0.f, 0.f, 0.f, 0.f};
     const int row16 = lane & 15, rq = lane >> 4;
@@ -855,11 +892,11 @@ wq_horner_pc_kg2_kernel(const __half *__restrict__ X, int M, int K, const uint32
     uint32_t w[4];
     float4 r4[2];
     half8_t a00, a01, a10, a11;
-    half8_t bP[4], bQ[4];
-    auto read_bh = [&](half8_t (&b)[4], const uint8_t *sx, int h, int hb) __attribute__((always_inline)) {
+    half8_t bP[kHB], bQ[kHB];
+    auto read_bh = [&](half8_t (&b)[kHB], const uint8_t *sx, int h, int hb) __attribute__((always_inline)) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-            b[i] = *reinterpret_cast<const half8_t *>(sx + soff[h] + (4 * hb + i) * 16 * kBK * 2);
+        for (int i = 0; i < kHB; ++i)
+            b[i] = *reinterpret_cast<const half8_t *>(sx + soff[h] + (kHB * hb + i) * 16 * kBK * 2);
     };
     auto make_a = [&](int h, half8_t &c0, half8_t &c1) __attribute__((always_inline)) {
         u32x4p_t u0 = __builtin_bit_cast(u32x4p_t, dequant_exact<4>(w, 2 * h, ec));
@@ -886,7 +923,7 @@ wq_horner_pc_kg2_kernel(const __half *__restrict__ X, int M, int K, const uint32
         }
     };
     // half hb of substep h (32-deep half h of the k-step): 8 MFMAs on bc beside the next half's reads
-    auto half_step = [&](const uint8_t *sx, half8_t (&bc)[4], half8_t (&bn)[4], int h, int hb, bool gf)
+    auto half_step = [&](const uint8_t *sx, half8_t (&bc)[kHB], half8_t (&bn)[kHB], int h, int hb, bool gf)
         __attribute__((always_inline)) {
         const half8_t &a0 = h ? a10 : a00;
         const half8_t &a1 = h ? a11 : a01;
@@ -897,27 +934,27 @@ wq_horner_pc_kg2_kernel(const __half *__restrict__ X, int M, int K, const uint32
         if (hb == 0 && h == 0) make_a(1, a10, a11);
         if (gf && h == 0) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                rescale(4 * hb + i);
-                mma(4 * hb + i, 0, a0, bc[i]);
-                mma(4 * hb + i, 1, a1, bc[i]);
+            for (int i = 0; i < kHB; ++i) {
+                rescale(kHB * hb + i);
+                mma(kHB * hb + i, 0, a0, bc[i]);
+                mma(kHB * hb + i, 1, a1, bc[i]);
             }
             __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                if (i + 1 < 4) __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+            for (int i = 0; i < kHB; ++i) {
+                if (i + 1 < kHB) __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
                 __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
                 __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                 __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
             }
         } else {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                mma(4 * hb + i, 0, a0, bc[i]);
-                mma(4 * hb + i, 1, a1, bc[i]);
+            for (int i = 0; i < kHB; ++i) {
+                mma(kHB * hb + i, 0, a0, bc[i]);
+                mma(kHB * hb + i, 1, a1, bc[i]);
             }
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
+            for (int i = 0; i < kHB; ++i) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
                 __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
                 __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
@@ -928,14 +965,14 @@ wq_horner_pc_kg2_kernel(const __half *__restrict__ X, int M, int K, const uint32
     };
     auto step = [&](int slot, auto gf_tag) __attribute__((always_inline)) {
         constexpr bool GF = decltype(gf_tag)::value;
-        const uint8_t *sb = smem + slot * kK2Stage;
-        const uint8_t *sx = sb + kg * kPcXSub;
+        const uint8_t *sb = smem + slot * L::kStage;
+        const uint8_t *sx = sb + kg * L::kXSub;
         {
-            const uint4 v = *reinterpret_cast<const uint4 *>(sb + kK2XB + kg * 4096 + nw * 1024 + lane * 16);
+            const uint4 v = *reinterpret_cast<const uint4 *>(sb + L::kXB + kg * 4096 + nw * 1024 + lane * 16);
             w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
         }
         if constexpr (GF) {
-            const uint8_t *gb = sb + kK2XB + kK2W + kg * 2048;
+            const uint8_t *gb = sb + L::kXB + L::kW + kg * 2048;
             half2_t nz, sc;
             split_sz(*reinterpret_cast<const uint32_t *>(gb + (nw * 32 + (lane & 31)) * 4), nz, sc);
             ec = exact_consts(nz);
@@ -988,62 +1025,80 @@ wq_horner_pc_kg2_kernel(const __half *__restrict__ X, int M, int K, const uint32
     for (int cb = 0; cb < 2; ++cb) {
         const float4 sv = *reinterpret_cast<const float4 *>(sl + 16 * cb);
 #pragma unroll
-        for (int t = 0; t < 8; ++t) {
+        for (int t = 0; t < TB; ++t) {
             acc[t][cb][0] *= sv.x;
             acc[t][cb][1] *= sv.y;
             acc[t][cb][2] *= sv.z;
             acc[t][cb][3] *= sv.w;
         }
     }
-    // k-group 1 -> LDS (the ring is drained); k-group 0 adds it (P0 + P1, a fixed order)
-    if (kg == 1) {
+    // The halves' sums through LDS (the ring is drained): k-group 0 finalizes token blocks
+    // [0, TB/2), k-group 1 blocks [TB/2, TB); each hands the other's blocks over and adds the ones
+    // it receives (P0 + P1: IEEE addition commutes, so either side's sum is the same bits).
+    constexpr int kT0 = TB / 2;
+    const int t_own = kg * kT0;   // first own block
+    auto hand_off = [&](auto off_tag) __attribute__((always_inline)) {   // the other k-group's blocks
+        constexpr int off = decltype(off_tag)::value;
 #pragma unroll
-        for (int t = 0; t < 8; ++t)
+        for (int i = 0; i < kT0; ++i)
 #pragma unroll
             for (int cb = 0; cb < 2; ++cb)
-                part[((nw * 8 + t) * 2 + cb) * 64 + lane] =
-                    make_float4(acc[t][cb][0], acc[t][cb][1], acc[t][cb][2], acc[t][cb][3]);
-    }
+                part[((nw * TB + off + i) * 2 + cb) * 64 + lane] =
+                    make_float4(acc[off + i][cb][0], acc[off + i][cb][1], acc[off + i][cb][2], acc[off + i][cb][3]);
+    };
+    if (kg == 0) hand_off(std::integral_constant<int, kT0>{});
+    else hand_off(std::integral_constant<int, 0>{});
     __syncthreads();
-    if (kg == 1) {
-        if constexpr (kHalfY) {
-            if (full) {
-                __syncthreads();
-                const int c = lane & 15;
-                for (int i = wave; i < kPcRows / 4; i += kPcCons + kPcProd) {
-                    const int t = 4 * i + (lane >> 4);
-                    const uint4 v = *reinterpret_cast<const uint4 *>(img + t * 256 + ((c ^ (t & 15)) * 16));
-                    typedef unsigned int u4nt __attribute__((ext_vector_type(4)));
-                    __builtin_nontemporal_store(u4nt{v.x, v.y, v.z, v.w},
-                                                reinterpret_cast<u4nt *>(Y + static_cast<size_t>(m0 + t) * N + n0 + 8 * c));
-                }
-            }
-        }
-        return;
-    }
     float4 bv[2];
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-        bv[cb] = *reinterpret_cast<const float4 *>(bias + nc0 + 16 * cb);
+    for (int cb = 0; cb < 2; ++cb) bv[cb] = *reinterpret_cast<const float4 *>(bias + nc0 + 16 * cb);
+    fx4p_t fin[kT0][2];   // the own blocks' sums
+    // (each k-group's branch indexes acc with constants: a run-time index would put acc in scratch)
+    auto finalize = [&](auto off_tag) __attribute__((always_inline)) {
+        constexpr int off = decltype(off_tag)::value;
 #pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            const float4 o = part[((nw * 8 + t) * 2 + cb) * 64 + lane];
-            acc[t][cb][0] = acc[t][cb][0] + o.x;
-            acc[t][cb][1] = acc[t][cb][1] + o.y;
-            acc[t][cb][2] = acc[t][cb][2] + o.z;
-            acc[t][cb][3] = acc[t][cb][3] + o.w;
-        }
-    }
-    if constexpr (EPI == 1) {
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            const int m = m0 + 16 * t + row16;
-            if (m >= M) continue;
+        for (int i = 0; i < kT0; ++i)
 #pragma unroll
             for (int cb = 0; cb < 2; ++cb) {
-                if (nc0 + 16 * cb >= N) continue;
-                psample4(epi, m, nc0 + 16 * cb, N, acc[t][cb][0] + bv[cb].x, acc[t][cb][1] + bv[cb].y,
-                         acc[t][cb][2] + bv[cb].z, acc[t][cb][3] + bv[cb].w);
+                const float4 o = part[((nw * TB + off + i) * 2 + cb) * 64 + lane];
+                fin[i][cb] = fx4p_t{acc[off + i][cb][0] + o.x, acc[off + i][cb][1] + o.y, acc[off + i][cb][2] + o.z,
+                                    acc[off + i][cb][3] + o.w};
+            }
+    };
+    if (kg == 0) finalize(std::integral_constant<int, 0>{});
+    else finalize(std::integral_constant<int, kT0>{});
+    if constexpr (EPI == 1) {
+        // block i + 1's x_t values and row coefficients are loaded before block i's stores (psample4_x)
+        float4 xa[2], xn[2];
+        float ca[3], cn[3];
+        auto load_blk = [&](int t, float4 (&x)[2], float (&c)[3]) __attribute__((always_inline)) {
+            const int m = m0 + 16 * t + row16;
+            const bool mok = m < M;
+            const float *cp = epi.coef + 3 * ((mok ? m : 0) / epi.rps);
+            c[0] = cp[0]; c[1] = cp[1]; c[2] = cp[2];
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb)
+                x[cb] = mok && nc0 + 16 * cb < N
+                            ? *reinterpret_cast<const float4 *>(epi.x_t + static_cast<size_t>(m) * N + nc0 + 16 * cb)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+        };
+        load_blk(t_own, xa, ca);
+#pragma unroll
+        for (int i = 0; i < kT0; ++i) {
+            if (i + 1 < kT0) load_blk(t_own + i + 1, xn, cn);
+            const int m = m0 + 16 * (t_own + i) + row16;
+            if (m < M) {
+#pragma unroll
+                for (int cb = 0; cb < 2; ++cb) {
+                    if (nc0 + 16 * cb >= N) continue;
+                    psample4_x(epi, static_cast<size_t>(m) * N + nc0 + 16 * cb, xa[cb], ca[0], ca[1], ca[2],
+                               fin[i][cb][0] + bv[cb].x, fin[i][cb][1] + bv[cb].y, fin[i][cb][2] + bv[cb].z,
+                               fin[i][cb][3] + bv[cb].w);
+                }
+            }
+            if (i + 1 < kT0) {
+                xa[0] = xn[0]; xa[1] = xn[1];
+                ca[0] = cn[0]; ca[1] = cn[1]; ca[2] = cn[2];
             }
         }
         return;
@@ -1051,22 +1106,22 @@ wq_horner_pc_kg2_kernel(const __half *__restrict__ X, int M, int K, const uint32
     if constexpr (kHalfY) {
         if (full) {
 #pragma unroll
-            for (int t = 0; t < 8; ++t) {
-                const int r = 16 * t + row16;
+            for (int i = 0; i < kT0; ++i) {
+                const int r = 16 * (t_own + i) + row16;
 #pragma unroll
                 for (int cb = 0; cb < 2; ++cb) {
                     const int pc = (4 * nw + 2 * cb + (rq >> 1)) ^ (r & 15);
                     union { __half h[4]; uint2 u; } pk;
-                    pk.h[0] = __float2half_rn(acc[t][cb][0] + bv[cb].x);
-                    pk.h[1] = __float2half_rn(acc[t][cb][1] + bv[cb].y);
-                    pk.h[2] = __float2half_rn(acc[t][cb][2] + bv[cb].z);
-                    pk.h[3] = __float2half_rn(acc[t][cb][3] + bv[cb].w);
+                    pk.h[0] = __float2half_rn(fin[i][cb][0] + bv[cb].x);
+                    pk.h[1] = __float2half_rn(fin[i][cb][1] + bv[cb].y);
+                    pk.h[2] = __float2half_rn(fin[i][cb][2] + bv[cb].z);
+                    pk.h[3] = __float2half_rn(fin[i][cb][3] + bv[cb].w);
                     *reinterpret_cast<uint2 *>(img + r * 256 + pc * 16 + (rq & 1) * 8) = pk.u;
                 }
             }
             __syncthreads();
             const int c = lane & 15;
-            for (int i = wave; i < kPcRows / 4; i += kPcCons + kPcProd) {
+            for (int i = wave; i < L::kRows / 4; i += kPcCons + kPcProd) {
                 const int t = 4 * i + (lane >> 4);
                 const uint4 v = *reinterpret_cast<const uint4 *>(img + t * 256 + ((c ^ (t & 15)) * 16));
                 typedef unsigned int u4nt __attribute__((ext_vector_type(4)));
@@ -1078,14 +1133,14 @@ wq_horner_pc_kg2_kernel(const __half *__restrict__ X, int M, int K, const uint32
     }
     const bool vec_ok = (N % 4) == 0;
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-        const int m = m0 + 16 * t + row16;
+    for (int i = 0; i < kT0; ++i) {
+        const int m = m0 + 16 * (t_own + i) + row16;
         if (m >= M) continue;
         YT *yrow = Y + static_cast<size_t>(m) * N;
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
-            store_out4<YT>(yrow, bias, nc0 + 16 * cb, N, vec_ok, acc[t][cb][0], acc[t][cb][1], acc[t][cb][2],
-                           acc[t][cb][3]);
+            store_out4<YT>(yrow, bias, nc0 + 16 * cb, N, vec_ok, fin[i][cb][0], fin[i][cb][1], fin[i][cb][2],
+                           fin[i][cb][3]);
     }
 }
 
@@ -1111,23 +1166,33 @@ int launch_horner_pc_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
 }
 
 
-int launch_horner_pc_kg2_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
-    if (a.K % 256 != 0 || a.Npad % 128 != 0 || a.M < 1)
-        return fail(DLLM_ERR_SHAPE_MISMATCH, "Horner PC KG2 GEMM: needs K % 256 == 0 and Npad % 128 == 0");
-    const int nbm = (a.M + kPcRows - 1) / kPcRows, nbn = a.Npad / 128;
+template <int TB>
+int launch_pc_kg2_t(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
+    const int nbm = (a.M + K2L<TB>::kRows - 1) / K2L<TB>::kRows, nbn = a.Npad / 128;
     const unsigned nb = static_cast<unsigned>(nbm * nbn);
     const PSampleEpi ep = a.epi ? *a.epi : PSampleEpi{};
     if (a.epi)
-        wq_horner_pc_kg2_kernel<float, 1><<<nb, kPcThreads, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
-                                                                    a.epi->x_prev, a.N, a.Npad, nbm, nbn, ep);
+        wq_horner_pc_kg2_kernel<float, 1, TB><<<nb, kPcThreads, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
+                                                                        a.epi->x_prev, a.N, a.Npad, nbm, nbn, ep);
     else if (y_f32)
-        wq_horner_pc_kg2_kernel<float, 0><<<nb, kPcThreads, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
-                                                                    static_cast<float *>(a.Y), a.N, a.Npad, nbm, nbn, ep);
+        wq_horner_pc_kg2_kernel<float, 0, TB><<<nb, kPcThreads, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
+                                                                        static_cast<float *>(a.Y), a.N, a.Npad, nbm, nbn, ep);
     else
-        wq_horner_pc_kg2_kernel<__half, 0><<<nb, kPcThreads, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
-                                                                     static_cast<__half *>(a.Y), a.N, a.Npad, nbm, nbn, ep);
+        wq_horner_pc_kg2_kernel<__half, 0, TB><<<nb, kPcThreads, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
+                                                                         static_cast<__half *>(a.Y), a.N, a.Npad, nbm, nbn, ep);
     DLLM_LAUNCH_CHECK();
     return DLLM_OK;
+}
+
+int launch_horner_pc_kg2_gemm(const HornerGemmArgs &a, int rows, int y_f32, hipStream_t st) {
+    if (a.K % 256 != 0 || a.Npad % 128 != 0 || a.M < 1)
+        return fail(DLLM_ERR_SHAPE_MISMATCH, "Horner PC KG2 GEMM: needs K % 256 == 0 and Npad % 128 == 0");
+    switch (rows) {
+    case 128: return launch_pc_kg2_t<8>(a, y_f32, st);
+    case 64: return launch_pc_kg2_t<4>(a, y_f32, st);
+    case 32: return launch_pc_kg2_t<2>(a, y_f32, st);
+    default: return fail(DLLM_ERR_UNSUPPORTED, "Horner PC KG2 GEMM: tile rows must be 128, 64 or 32");
+    }
 }
 
 }  // namespace dllm

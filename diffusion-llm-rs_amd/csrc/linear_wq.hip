@@ -1424,28 +1424,38 @@ bool horner_pc_ready(const dllm_linear *hc, int M, hipStream_t st) {
 #endif
 }
 
-// The two-k-group PC kernel (128 x 128 tiles, linear_pc.hip): where none of the larger Horner grids
-// fills a round and 128 x 128 tiles fill exactly one (the 4-GPU column shard M = 4096 x N 1024;
-// M = 2048 x N 2048; M = 1024 x N 4096).
+// The two-k-group PC kernel (rows x 128 tiles, linear_pc.hip): where none of the larger Horner grids
+// fills a round, the largest rows in {128, 64} whose grid fills exactly one round (128: the 4-GPU
+// column shard M = 4096 x N 1024, M = 2048 x N 2048, M = 1024 x N 4096: 34.8 -> 32.3 us; 64: M = 512
+// x N 4096 and the 8-GPU shard 4096 x 512: 22.1 -> 21.5 us).  32-row tiles (DLLM_PC_KG2_SMALL, A/B)
+// lose to the 4-k-group fold tiles at mid M (M 256: 17.1 vs 14.3 us; profiles/r06_tiles/).  Returns
+// the tile rows, 0 = not applicable.
 #ifndef DLLM_HORNER_PC_KG2
 #define DLLM_HORNER_PC_KG2 1
 #endif
+#ifndef DLLM_PC_KG2_SMALL   // 64- and 32-token tiles too
+#define DLLM_PC_KG2_SMALL 0
+#endif
 bool horner_kg2_ready(const dllm_linear *hc, int M);
-bool horner_pc_kg2_ready(const dllm_linear *hc, int M, hipStream_t st) {
+int horner_pc_kg2_rows(const dllm_linear *hc, int M, hipStream_t st) {
 #if DLLM_HORNER_PC_KG2
     const int np = static_cast<int>(hc->Npad);
     if (!(hc->precision == DLLM_PRECISION_EXACT && hc->bits == 4 && hc->group == 128 && hc->K % 256 == 0 &&
           np % 128 == 0 && hc->hstate == 1))
-        return false;
+        return 0;
 #if DLLM_LAB
-    if (hc->variant == 14 || hc->variant == 28) return false;   // lab A/B: the fold-form exact policy
+    if (hc->variant == 14 || hc->variant == 28) return 0;   // lab A/B: the fold-form exact policy
 #endif
-    const int t128 = ((M + 127) / 128) * (np / 128);
-    return t128 >= kCUs && t128 < 2 * kCUs && !horner_ready(hc, M, st) && !horner_pc_ready(hc, M, st) &&
-           !horner_kg2_ready(hc, M);
+    if (horner_ready(hc, M, st) || horner_pc_ready(hc, M, st) || horner_kg2_ready(hc, M)) return 0;
+    for (int rows = 128; rows >= (DLLM_PC_KG2_SMALL ? 32 : 64); rows /= 2) {
+        const int t = ((M + rows - 1) / rows) * (np / 128);
+        if (t >= 2 * kCUs) return 0;   // the next larger tile already had a full round
+        if (t >= kCUs) return rows;
+    }
+    return 0;
 #else
     (void)hc; (void)M; (void)st;
-    return false;
+    return 0;
 #endif
 }
 
@@ -1519,10 +1529,10 @@ int launch_prefill_auto(const dllm_linear *h, const __half *X, int M, YT *Y, hip
                                    (int)h->Npad, epi};
             return launch_horner_kg2_gemm(a, std::is_same<YT, float>::value ? 1 : 0, st);
         }
-        if (BITS == 4 && horner_pc_kg2_ready(h, M, st)) {
+        if (const int rows = BITS == 4 ? horner_pc_kg2_rows(h, M, st) : 0) {
             const HornerGemmArgs a{X, M, (int)h->K, h->wdev, h->sz, h->hr, h->sf, h->bias, Y, (int)h->N,
                                    (int)h->Npad, epi};
-            return launch_horner_pc_kg2_gemm(a, std::is_same<YT, float>::value ? 1 : 0, st);
+            return launch_horner_pc_kg2_gemm(a, rows, std::is_same<YT, float>::value ? 1 : 0, st);
         }
 #if DLLM_LAB
         if (const int rows = BITS == 4 ? horner_rows(h, M) : 0) {   // lab A/B 323 only

@@ -930,14 +930,18 @@ def test_linear_staggered_tiles_exact_integers(dllm, torch, K):
 
 
 @pytest.mark.parametrize("K", [256, 512, 768, 2304])
-@pytest.mark.parametrize("M,N", [(4096, 1024), (2048, 2048), (1024, 4096), (1000, 4096), (4096, 1020)])
+@pytest.mark.parametrize("M,N", [(4096, 1024), (2048, 2048), (1024, 4096), (1000, 4096), (4096, 1020),
+                                 (512, 4096), (4096, 512), (500, 4096), (256, 4096), (300, 4096)])
 def test_linear_pc_kg2_tiles_exact_integers(dllm, torch, K, M, N):
-    """The two-k-group producer/consumer kernel (linear_pc.hip, 128 x 128 tiles: the 4-GPU column
-    shard 4096 x 1024, 2048 x 2048, 1024 x 4096) on exact-integer data, bit-equal to the f64 product
-    for f32 and f16 outputs: K-half kg's Horner chain in k-group kg, the halves' partials summed in
-    a fixed order.  K 256 .. 2304 = 1 .. 9 groups per half (a ring period of 3 stages that does not
-    divide the 2 .. 18 k-steps of a half); M 1000 leaves a ragged last row block, N 1020 a padded
-    last column block (the 8-B row-store path)."""
+    """The two-k-group producer/consumer kernel (linear_pc.hip) on exact-integer data, bit-equal to
+    the f64 product for f32 and f16 outputs: K-half kg's Horner chain in k-group kg, the halves'
+    partials summed through LDS (each k-group finalizes half the token blocks).  Tiles of 128 x 128
+    (the 4-GPU column shard 4096 x 1024, 2048 x 2048, 1024 x 4096) and 64 x 128 (M 512 / 500 at N
+    4096, the 8-GPU shard 4096 x 512); M 256 / 300 take the 4-k-group fold tiles of mid M (the
+    32 x 128 PC tiles are an A/B build only).  K 256 .. 2304 = 1 .. 9 groups
+    per half (a ring period of 3 stages that does not divide the 2 .. 18 k-steps of a half); M
+    1000 / 500 / 300 leave a ragged last row block, N 1020 a padded last column block (the 8-B
+    row-store path)."""
     rng = np.random.default_rng(K + M + N)
     W = rng.integers(0, 16, (K, N)).astype(np.float32)
     for g0 in range(0, K, 128):
