@@ -601,6 +601,10 @@ kv_attention5_kernel(const _Float16 *__restrict__ Q, const uint8_t *__restrict__
 }
 
 
+#if DLLM_LAB   // producer/consumer attention (A/B against v5; measured slower, profiles/r06_attn/)
+#include "lab/attn_pc.inc"
+#endif
+
 #if DLLM_LAB   // attention on 16x16x32 MFMAs (A/B against v5)
 #include "lab/attn16.inc"
 #endif
@@ -686,6 +690,9 @@ extern "C" int dllm_kv_attention(const void *Q, const uint8_t *Kq, const float *
             break;
         case 612:   // the product without the region-1 softmax pins (A/B; bit-identical)
             kv_attention5_kernel<512, false><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh);
+            break;
+        case 700:   // the producer/consumer kernel (A/B; bit-identical)
+            kv_attention_pc_kernel<<<grid, kPcAttnWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh);
             break;
         case 198:   // the staggered schedule (A/B; bit-identical)
             kv_attention5_kernel<0, true><<<grid, kWaves * 64, 0, st>>>(Qh, img, k_params, v_params, (int)S, (int)H, Oh);
