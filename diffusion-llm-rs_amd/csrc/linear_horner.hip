@@ -602,6 +602,7 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
         c0 = __builtin_bit_cast(half8_t, u0);
         c1 = __builtin_bit_cast(half8_t, u1);
     };
+    bool a_done = false;   // MODE bit 3 (lab ablation): the A fragments are built in the first step only
     // MODE bit 8: the pending stage's pieces, issued between MFMA quarters of substeps 2 and 3
     int pend_slot = 0, pend_st = 0;
     bool pend_gf = false, pend_on = false;
@@ -627,7 +628,7 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
         const half8_t &a0 = use1 ? a10 : a00;
         const half8_t &a1 = use1 ? a11 : a01;
         __builtin_amdgcn_sched_barrier(0);
-        if ((MODE & 1024) == 0 && TB == 16 && j == 2) {   // lab A/B: half 1's A fragments at substep 2
+        if ((MODE & 1024) == 0 && TB == 16 && j == 2 && !((MODE & 8) && a_done)) {   // lab A/B: half 1's A fragments at substep 2
             make_a(1, a10, a11);
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -671,7 +672,7 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
             // rescale beside block i's MFMAs)
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
-                rescale(tb0 + i);
+                if constexpr ((MODE & 4) == 0) rescale(tb0 + i);   // (bit 2: lab ablation, no rescale)
                 mma(tb0 + i, 0, a0, bc[i]);
                 mma(tb0 + i, 1, a1, bc[i]);
             }
@@ -720,7 +721,7 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
     // opens a group (every stage at TB = 8; TB = 16: even k-steps, so si + 2 opens one iff si does).
     auto step = [&](int slot, int si, auto gf_tag) __attribute__((always_inline)) {
         constexpr bool GF = decltype(gf_tag)::value;
-        const bool issue = si + 2 < ns;
+        const bool issue = (MODE & 64) == 0 && si + 2 < ns;   // (bit 6: lab ablation, no DMA after the prologue)
         if (!STAG && issue) stage((slot + 2) % 3, si + 2, GF);
         const uint8_t *sb = smem + slot * kStage;
         // MODE bit 11 (TB = 16): a non-group-first step's words and half-0 A fragments were built at
@@ -737,15 +738,16 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
             r4[1] = *reinterpret_cast<const float4 *>(rl + 16);
         }
         read_b(bA, sb, 0);
-        if (!(kEarly && !GF)) make_a(0, a00, a01);
+        if (!(kEarly && !GF) && !((MODE & 8) && a_done)) make_a(0, a00, a01);   // (bit 3: lab ablation, A once)
         sub(sb, bA, bB, 0, GF);
         sub(sb, bB, bA, 1, GF);
         if constexpr (TB == 16 && (MODE & 1024) != 0) {
             // half 1's A fragments right behind substep 1's MFMAs (their registers free once those
             // issue): the dequant runs while the MFMAs drain and the wave reaches the barrier
-            make_a(1, a10, a11);
+            if (!((MODE & 8) && a_done)) make_a(1, a10, a11);
             __builtin_amdgcn_sched_barrier(0);
         }
+        if constexpr ((MODE & 8) != 0) a_done = true;
         if constexpr (STAG) {
             if (grp_b) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             barrier();
