@@ -844,7 +844,7 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
         return;
     }
     const bool full = (m0 + 16 * TB <= M) && (n0 + 256 <= N) && (N % 4) == 0;
-    if constexpr (std::is_same<YT, __half>::value) {
+    if constexpr (std::is_same<YT, __half>::value && (MODE & 4096) == 0) {   // (bit 12, lab A/B: 8-B stores from registers)
         if (full && (N % 8) == 0) {   // coalesced 16-B row stores through the drained ring
             store_tile16_f16_lds<TB>(smem, acc, bv, Y, N, m0, n0, wave, lane);
             return;

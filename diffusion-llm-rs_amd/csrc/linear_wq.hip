@@ -1488,7 +1488,7 @@ int launch_horner(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream
     if (h->variant >= 310 && h->variant <= 312) a.lab = h->variant - 300;   // lab XCD groupings (10..12)
     if ((h->variant >= 314 && h->variant <= 321) || (h->variant >= 324 && h->variant <= 328)) a.lab = h->variant - 300;   // lab: MFMA only / DMA only / burst DMA / ...
     if (h->variant == 305) a.lab = 7;   // lab ablation: no stores, rescale; one dequant and B read per k-step
-    if (h->variant >= 340 && h->variant <= 343) a.lab = h->variant - 300;   // product-kernel ablations (40..43)
+    if (h->variant >= 340 && h->variant <= 345) a.lab = h->variant - 300;   // product-kernel ablations / A/B (40..45)
 #endif
     return launch_horner_gemm(a, std::is_same<YT, float>::value ? 1 : 0, st);
 }
@@ -1956,8 +1956,8 @@ int dllm_linear_set_kernel_variant(dllm_linear_t h, int variant) {
         return DLLM_OK;
     }
     if (variant < -1 || (variant > 15 && (variant < 24 || variant > 31) && (variant < 300 || variant > 331 || variant == 313) &&
-                         (variant < 340 || variant > 343)))
-        return fail(DLLM_ERR_INVALID_PARAMS, "variant must be -1..15, 24..31, 300..312, 314..331 or 340..343 (16..23, 32..95, 100..195, 200..263: ablations)");
+                         (variant < 340 || variant > 345)))
+        return fail(DLLM_ERR_INVALID_PARAMS, "variant must be -1..15, 24..31, 300..312, 314..331 or 340..345 (16..23, 32..95, 100..195, 200..263: ablations)");
     h->variant = variant;
     h->dlab = h->rlab = h->pplab = h->dcfg = 0;
     return DLLM_OK;
