@@ -62,9 +62,9 @@ def parse():
                    help="N > 1: steps of the hidden-dim-sharded C5 loop reported as 'denoise_loop_tp' (0 skips)")
     p.add_argument("--dp-steps", type=int, default=50,
                    help="N > 1: steps of the token-parallel C5 loop reported as 'denoise_loop_dp' (0 skips)")
-    p.add_argument("--gather-chunks", type=int, default=1,
+    p.add_argument("--gather-chunks", type=int, default=2,
                    help="N > 1: token chunks of the headline step's all-gather (chunk i's gather overlaps "
-                        "chunk i+1's GEMM)")
+                        "chunk i+1's GEMM; 2 by default: priced in DESIGN.md section 6)")
     p.add_argument("--no-denoise", action="store_true",
                    help="skip the config-C5 denoise-loop side measurement (reported as 'denoise_loop')")
     p.add_argument("--prewarm-ms", type=float, default=300.0,
