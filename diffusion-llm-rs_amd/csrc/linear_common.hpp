@@ -348,6 +348,7 @@ struct HornerGemmArgs {
     int N, Npad;
     const PSampleEpi *epi;
     int lab = 0;   // lab build only: 1 = the unstaggered schedule (A/B); 2 / 3 = staggered / not, no stores
+    int bits = 4;  // launch_horner_gemm: int4 or int2 codes (the other Horner launchers: int4 only)
 };
 int launch_horner_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st);
 // The same kernel on 128- or 64-token x 256-column tiles (rows = 128 / 64: grids where larger tiles

@@ -485,13 +485,18 @@ struct H16 {
     static constexpr int kPieces = kKPS * (kNX + 1) + 1;   // DMA pieces per stage (X, W, group data)
 };
 
-template <typename YT, int EPI, int MODE, int TB = 16>
+template <typename YT, int EPI, int MODE, int TB = 16, int BITS = 4>
 __global__ void __launch_bounds__(512, 1)
 wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *__restrict__ wdev,
                    const uint32_t *__restrict__ sz, const float *__restrict__ hr, const float *__restrict__ sf,
                    const float *__restrict__ bias, YT *__restrict__ Y, int N, int Npad, int nbm, int nbn,
                    PSampleEpi epi) {
     constexpr bool STAG = MODE & 1;
+    // BITS = 2 (int2 g128, 256-token tiles only): a wave's weight words of the k-step pair (2u, 2u + 1)
+    // are one 1-KiB piece of the code layout (k-step 2u's 64 lanes x 8 B, then 2u + 1's); every stage
+    // moves its pair's piece (twice per pair: int2's 4 MiB of words at 4096^2 read twice, the int4
+    // stage's bytes) and reads its own half, so the ring, the pieces per stage and the waits are int4's.
+    static_assert(BITS == 4 || (BITS == 2 && TB == 16), "int4, or int2 on 256-token tiles");
     using L = H16<TB>;
     constexpr int kStage = L::kStage, kXB = L::kXB, kKPS = L::kKPS;
     __shared__ __attribute__((aligned(16))) uint8_t smem[3 * kStage];
@@ -517,7 +522,8 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
     }
     const __amdgpu_buffer_rsrc_t xr = raw_rsrc(X + static_cast<size_t>(m0) * K);
     const uint32_t nt = static_cast<uint32_t>(n0 + 32 * wave) >> 5;
-    const __amdgpu_buffer_rsrc_t wr = raw_rsrc(wdev + static_cast<size_t>(nt) * nk * 64 * 4);
+    const __amdgpu_buffer_rsrc_t wr = raw_rsrc(wdev + static_cast<size_t>(nt) * nk * 64 * BITS);
+    auto wsoff = [](int kstep) { return static_cast<uint32_t>(BITS == 4 ? kstep * 1024 : (kstep & ~1) * 512); };
     const uint32_t wo = static_cast<uint32_t>(lane * 16);
     const __amdgpu_buffer_rsrc_t gr =
         raw_rsrc(wave == 0 ? static_cast<const void *>(sz + n0) : static_cast<const void *>(hr + n0));
@@ -535,7 +541,7 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
                        base + static_cast<uint32_t>(kk * L::kXSub + wave * 1024 + i * 0x2000));
         } else if (p < nxp + kKPS) {
             const int kk = p - nxp;
-            blds16_asm(wr, wo, static_cast<uint32_t>((st * kKPS + kk) * 1024),
+            blds16_asm(wr, wo, wsoff(st * kKPS + kk),
                        base + static_cast<uint32_t>(kXB + kk * kHW + wave * 1024));
         } else if (p == nxp + kKPS && gf && has_g) {
             blds16_asm(gr, wo, static_cast<uint32_t>(((st * kKPS) >> 1) * Npad * 4),
@@ -545,7 +551,7 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
     auto stage = [&](int slot, int st, bool gf) __attribute__((always_inline)) {
         if constexpr (TB == 16) {
             horner_burst(xr, xo[0], xo[1], xo[2], xo[3], static_cast<uint32_t>(st * kBK * 2), wr, wo,
-                         static_cast<uint32_t>(st * 1024), sbase + static_cast<uint32_t>(slot * kStage + wave * 1024));
+                         wsoff(st), sbase + static_cast<uint32_t>(slot * kStage + wave * 1024));
             piece(L::kPieces - 1, slot, st, gf);
         } else {
 #pragma unroll
@@ -582,17 +588,24 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
     };
 
     ExactConsts ec;
-    uint32_t w[4];
+    uint32_t w[BITS];
     float4 r4[2];
     half8_t bA[8], bB[8], a00, a01, a10, a11;
-    auto load_w = [&](const uint8_t *sb, int kk) __attribute__((always_inline)) {
-        const uint4 v = *reinterpret_cast<const uint4 *>(sb + kXB + kk * kHW + wave * 1024 + lane * 16);
-        w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+    // par: the k-step's parity (BITS = 2: which half of the pair's piece)
+    auto load_w = [&](const uint8_t *sb, int kk, int par) __attribute__((always_inline)) {
+        if constexpr (BITS == 4) {
+            (void)par;
+            const uint4 v = *reinterpret_cast<const uint4 *>(sb + kXB + kk * kHW + wave * 1024 + lane * 16);
+            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+        } else {
+            const uint2 v = *reinterpret_cast<const uint2 *>(sb + kXB + kk * kHW + wave * 1024 + par * 512 + lane * 8);
+            w[0] = v.x; w[1] = v.y;
+        }
     };
     // A fragments of half h (words 2h, 2h + 1) for column blocks 0 and 1
     auto make_a = [&](int h, half8_t &c0, half8_t &c1) __attribute__((always_inline)) {
-        u32x4_t u0 = __builtin_bit_cast(u32x4_t, dequant_exact<4>(w, 2 * h, ec));
-        u32x4_t u1 = __builtin_bit_cast(u32x4_t, dequant_exact<4>(w, 2 * h + 1, ec));
+        u32x4_t u0 = __builtin_bit_cast(u32x4_t, dequant_exact<BITS>(w, 2 * h, ec));
+        u32x4_t u1 = __builtin_bit_cast(u32x4_t, dequant_exact<BITS>(w, 2 * h + 1, ec));
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const auto r = __builtin_amdgcn_permlane16_swap(u0[e], u1[e], false, false);
@@ -632,7 +645,7 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
             make_a(1, a10, a11);
             __builtin_amdgcn_sched_barrier(0);
         }
-        if (TB == 8 && j == 1) load_w(sb, 1);   // k-step 1's words (k-step 0's last use was in substep 0)
+        if (TB == 8 && j == 1) load_w(sb, 1, 1);   // k-step 1's words (k-step 0's last use was in substep 0)
         __builtin_amdgcn_s_setprio(1);
         if (TB == 8 && j < 3) {   // the next substep's A fragments beside this substep's MFMAs
             if (j & 1) make_a(0, a00, a01);
@@ -728,7 +741,7 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
         // the end of the step before (the wave's own weight-word DMA is complete after its vmcnt
         // wait; the zero points are the group's), so they overlap that step's MFMA drain
         constexpr bool kEarly = (MODE & 2048) != 0 && TB == 16;
-        if (!(kEarly && !GF)) load_w(sb, 0);
+        if (!(kEarly && !GF)) load_w(sb, 0, si & 1);
         if constexpr (GF) {
             half2_t nz, sc;
             split_sz(*reinterpret_cast<const uint32_t *>(sb + kXB + L::kWB + (wave * 32 + (lane & 31)) * 4), nz, sc);
@@ -768,7 +781,7 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
         }
         if constexpr (kEarly && GF) {   // the next (same-group) step's words and half-0 A fragments
             __builtin_amdgcn_sched_barrier(0);
-            load_w(smem + ((slot + 1) % 3) * kStage, 0);
+            load_w(smem + ((slot + 1) % 3) * kStage, 0, (si + 1) & 1);
             make_a(0, a00, a01);
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -874,19 +887,19 @@ wq_horner16_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *_
     }
 }
 
-template <int MODE, int TB = 16>
+template <int MODE, int TB = 16, int BITS = 4>
 void launch_horner16_t(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
     const int nbm = (a.M + 16 * TB - 1) / (16 * TB), nbn = a.Npad / 256;
     const unsigned nb = static_cast<unsigned>(nbm * nbn);
     const PSampleEpi ep = a.epi ? *a.epi : PSampleEpi{};
     if (a.epi)
-        wq_horner16_kernel<float, 1, MODE, TB><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
+        wq_horner16_kernel<float, 1, MODE, TB, BITS><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
                                                                a.epi->x_prev, a.N, a.Npad, nbm, nbn, ep);
     else if (y_f32)
-        wq_horner16_kernel<float, 0, MODE, TB><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
+        wq_horner16_kernel<float, 0, MODE, TB, BITS><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
                                                                static_cast<float *>(a.Y), a.N, a.Npad, nbm, nbn, ep);
     else
-        wq_horner16_kernel<__half, 0, MODE, TB><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
+        wq_horner16_kernel<__half, 0, MODE, TB, BITS><<<nb, 512, 0, st>>>(a.X, a.M, a.K, a.wdev, a.sz, a.hr, a.sf, a.bias,
                                                                 static_cast<__half *>(a.Y), a.N, a.Npad, nbm, nbn, ep);
 }
 
@@ -915,9 +928,10 @@ int launch_horner_kg2_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
 
 int launch_horner_gemm(const HornerGemmArgs &a, int y_f32, hipStream_t st) {
 #if DLLM_LAB
-    if (a.lab) return launch_horner_lab(a, y_f32, st);
+    if (a.lab && a.bits == 4) return launch_horner_lab(a, y_f32, st);
 #endif
-    launch_horner16_t<1 | 256 | 1024>(a, y_f32, st);
+    if (a.bits == 2) launch_horner16_t<1 | 256 | 1024, 16, 2>(a, y_f32, st);
+    else launch_horner16_t<1 | 256 | 1024>(a, y_f32, st);
     DLLM_LAUNCH_CHECK();
     return DLLM_OK;
 }

@@ -1346,9 +1346,10 @@ inline bool lab_horner128() {
 }
 #endif
 
+// int4 and (256 x 256 tiles only: horner_ready) int2 codes, group 128.
 inline bool horner_shape(const dllm_linear *h) {
-    return h->precision == DLLM_PRECISION_EXACT && h->bits == 4 && h->group == 128 && h->K % 128 == 0 &&
-           h->Npad % 256 == 0;
+    return h->precision == DLLM_PRECISION_EXACT && (h->bits == 4 || h->bits == 2) && h->group == 128 &&
+           h->K % 128 == 0 && h->Npad % 256 == 0;
 }
 
 // The handle's Horner ratios are valid (decided at create, immutable afterwards).
@@ -1379,7 +1380,7 @@ bool horner_ready(const dllm_linear *hc, int M, hipStream_t st) {
 #if DLLM_LAB
 int horner_rows(const dllm_linear *hc, int M) {
     const int np = static_cast<int>(hc->Npad);
-    if (hc->variant != 323 || !horner_shape(hc) || hc->hstate != 1) return 0;
+    if (hc->variant != 323 || hc->bits != 4 || !horner_shape(hc) || hc->hstate != 1) return 0;
     if (((M + 127) / 128) * (np / 256) >= kCUs) return 128;
     return 0;
 }
@@ -1412,7 +1413,7 @@ bool horner_kg2_ready(const dllm_linear *hc, int M) {
 bool horner_pc_ready(const dllm_linear *hc, int M, hipStream_t st) {
 #if DLLM_HORNER_PC
     const int np = static_cast<int>(hc->Npad);
-    if (!horner_shape(hc) || hc->hstate != 1) return false;
+    if (hc->bits != 4 || !horner_shape(hc) || hc->hstate != 1) return false;
 #if DLLM_LAB
     if (hc->variant == 14 || hc->variant == 28) return false;   // lab A/B: the fold-form exact policy
 #endif
@@ -1463,7 +1464,7 @@ template <typename YT, int EPI>
 int launch_horner(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream_t st, const PSampleEpi *epi) {
 #if DLLM_LAB
     const PSampleEpi ep = epi ? *epi : PSampleEpi{};
-    if (lab_horner128()) {
+    if (lab_horner128() && h->bits == 4) {
         const int nbm = (M + 127) / 128, nbn = static_cast<int>(h->Npad / 256);
         wq_gemm8_kernel<4, YT, 8, 4, false, 1, 0, EPI, true><<<static_cast<unsigned>(nbm * nbn), 512, 0, st>>>(
             X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn, 1, nullptr,
@@ -1471,7 +1472,7 @@ int launch_horner(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream
         DLLM_LAUNCH_CHECK();
         return DLLM_OK;
     }
-    if (h->variant == 24) {   // lab A/B: the round-2 Horner kernel (wq_gemm8_kernel<..., HORNER>)
+    if (h->variant == 24 && h->bits == 4) {   // lab A/B: the round-2 Horner kernel (wq_gemm8_kernel<..., HORNER>)
         const int nbm = (M + 255) / 256, nbn = static_cast<int>(h->Npad / 256);
         wq_gemm8_kernel<4, YT, 8, 8, false, 1, 0, EPI, true><<<static_cast<unsigned>(nbm * nbn), 512, 0, st>>>(
             X, M, (int)h->K, h->wdev, h->sz, h->bias, Y, (int)h->N, (int)h->Npad, (int)h->group, nbm, nbn, 1, nullptr,
@@ -1481,6 +1482,7 @@ int launch_horner(const dllm_linear *h, const __half *X, int M, YT *Y, hipStream
     }
 #endif
     HornerGemmArgs a{X, M, (int)h->K, h->wdev, h->sz, h->hr, h->sf, h->bias, Y, (int)h->N, (int)h->Npad, epi};
+    a.bits = static_cast<int>(h->bits);
 #if DLLM_LAB
     if (h->variant >= 25 && h->variant <= 27) a.lab = h->variant - 24;   // lab A/B (see HornerGemmArgs::lab)
     if (h->variant >= 29 && h->variant <= 31) a.lab = h->variant - 25;   // lab ablations 4..6
@@ -1519,7 +1521,7 @@ int launch_prefill_auto(const dllm_linear *h, const __half *X, int M, YT *Y, hip
     }
 #endif
     if (use_exact(h)) {
-        if (BITS == 4 && horner_ready(h, M, st)) return launch_horner<YT, EPI>(h, X, M, Y, st, epi);
+        if ((BITS == 4 || BITS == 2) && horner_ready(h, M, st)) return launch_horner<YT, EPI>(h, X, M, Y, st, epi);
         if (BITS == 4 && horner_pc_ready(h, M, st)) {
             const HornerGemmArgs a{X, M, (int)h->K, h->wdev, h->sz, h->hr, h->sf, h->bias, Y, (int)h->N,
                                    (int)h->Npad, epi};

@@ -1,7 +1,7 @@
 """A/B of library builds of the same ABI on the int4-g128 GEMM (default EXACT precision): each build
 in its own subprocess (DLLM_LIB=<file>), rounds interleaved, HIP events around 20 launches, median
 over rounds; a bit-level hash of Y shows whether two builds compute the same bits.
-Usage: LIBS=a.so,b.so [SHAPES=4096:4096,2048:4096] python scripts/gemm_ab.py   (measurement only)."""
+Usage: LIBS=a.so,b.so [SHAPES=4096:4096,2048:4096] [AB_BITS=4|2] python scripts/gemm_ab.py   (measurement only)."""
 import json, os, subprocess, sys
 from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
@@ -16,7 +16,7 @@ for sh in %r.split(","):
     M, N = (int(v) for v in sh.split(":"))
     torch.manual_seed(0)
     W = 0.02 * torch.randn(K, N, device="cuda")
-    lin = d.QuantLinear.from_weight(W, None, 4, 128)
+    lin = d.QuantLinear.from_weight(W, None, int(__import__("os").environ.get("AB_BITS", "4")), 128)
     X = torch.randn(M, K, device="cuda").half()
     Y = torch.empty(M, N, dtype=torch.float16, device="cuda")
     for _ in range(30): lin(X, out=Y)

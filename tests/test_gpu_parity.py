@@ -540,6 +540,37 @@ def test_linear_horner_scale_spread(dllm, torch, orc, spread, M, K):
     lin.close()
 
 
+@pytest.mark.parametrize("spread,M,K", [(8, 4096, 4096), (30, 4096, 2048), (45, 4096, 1024), (8, 8000, 1024),
+                                         (8, 4300, 1024)])
+def test_linear_horner_int2_scale_spread(dllm, torch, orc, spread, M, K):
+    """int2 g128 (config C3's int2 layers) on the 256 x 256-tile Horner kernel (wq_horner16_kernel
+    with BITS = 2: each stage moves its k-step pair's 1-KiB piece of weight words and reads its half),
+    the same per-column bound as the int4 case above against the f64 product of the same f16 X with
+    the reference's a2 weights; spread 45 rejects the ratios (fold-form kernel); M = 4300 takes the
+    fold form (its 256 x 256 grid needs too many rounds)."""
+    N, bits = 4096, 2
+    g = torch.Generator(device="cuda").manual_seed(7 * spread + M + K)
+    G = K // 128
+    mult = torch.exp2((torch.rand(G, N, device="cuda", generator=g) * 2 - 1) * spread)
+    W = 0.02 * torch.randn(K, N, device="cuda", generator=g) * mult.repeat_interleave(128, 0)
+    X = torch.randn(M, K, device="cuda", generator=g).half()
+    lin = dllm.QuantLinear.from_weight(W, None, bits, 128)
+    base = 2 * K * N * bits // 8 + G * N * 8 + N * 4   # code layouts (prefill, decode), sz + sf, bias
+    assert lin.device_bytes() == base + (0 if spread == 45 else (G + 1) * N * 4), (spread, lin.device_bytes())
+    codes, scales, zps = lin.export()
+    Wh = dev(torch, orc.dequantize_weights(orc.unpack_bits(host(codes), K * N, bits).reshape(K, N), host(scales),
+                                           host(zps), 128))
+    Yr = X.double() @ Wh.double()
+    for rep in range(2):
+        Y = lin(X, out_dtype=torch.float32).double()
+        assert torch.isfinite(Y).all()
+        col = torch.linalg.norm(Y - Yr, dim=0) / torch.linalg.norm(Yr, dim=0)
+        assert col.max().item() <= EXACT_TOL, (spread, rep, col.max().item())
+    Y16 = lin(X, out_dtype=torch.float16).double()
+    assert torch.equal(Y16, lin(X, out_dtype=torch.float32).half().double())
+    lin.close()
+
+
 @pytest.mark.parametrize("M,N,group", [(4096, 1024, 128), (4096, 512, 128), (1024, 4096, 128), (256, 4096, 256),
                                        (65, 4096, 128), (300, 1280, 64), (129, 384, 128)])
 def test_linear_split_k_combine_repeatable(dllm, torch, orc, M, N, group):
