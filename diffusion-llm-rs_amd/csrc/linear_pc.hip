@@ -31,6 +31,8 @@
 
 #include <type_traits>
 
+// DLLM_PC_ABL = 4 (128 x 256 kernel): the consumers build their A fragments in the first stage only (no
+// dequant VALU after it).
 // DLLM_PC_ABL (A/B builds only, results wrong, timing only): 1 = the producers issue no DMA after
 // the prologue (the consumers' compute + barriers alone); 2 = the consumers issue no MFMA (operands
 // kept live: loads + VALU + LDS reads + barriers); 3 = the consumers only join the barriers (the
@@ -227,7 +229,7 @@ wq_horner_pc_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *
             return v < 4 ? dequant_exact<4>(w0, v & 3, ec) : dequant_exact<4>(w1, v & 3, ec);
         };
         auto mma = [&](int r, const half8_t &a, const half8_t &b) __attribute__((always_inline)) {
-#if DLLM_PC_ABL >= 2
+#if DLLM_PC_ABL == 2 || DLLM_PC_ABL == 3
             asm volatile("" ::"v"(a), "v"(b));
             asm volatile("" : "+v"(acc[r]));
 #else
@@ -424,6 +426,7 @@ wq_horner_pc_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *
     float4 r4[2];
     half8_t a00, a01, a10, a11;
     half8_t bP[4], bQ[4];
+    bool a_done = false;
     // B fragments of token blocks 4 hb .. 4 hb + 3 of substep j (k-step j >> 1, half j & 1)
     auto read_bh = [&](half8_t (&b)[4], const uint8_t *sb, int j, int hb) __attribute__((always_inline)) {
 #pragma unroll
@@ -446,7 +449,7 @@ wq_horner_pc_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *
         c1 = __builtin_bit_cast(half8_t, u1);
     };
     auto mma = [&](int t, int cb, const half8_t &a, const half8_t &b) __attribute__((always_inline)) {
-#if DLLM_PC_ABL >= 2
+#if DLLM_PC_ABL == 2 || DLLM_PC_ABL == 3
         asm volatile("" ::"v"(a), "v"(b));
         asm volatile("" : "+v"(acc[t][cb]));
 #else
@@ -523,7 +526,7 @@ wq_horner_pc_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *
         __builtin_amdgcn_s_setprio(1);
         if (hb == 0) read_bh(bn, sb, j, 1);
         else if (j < 3) read_bh(bn, sb, j + 1, 0);
-        if (hb == 0 && j < 3) {   // the next substep's A fragments (its half is the other one)
+        if (hb == 0 && j < 3 && !(DLLM_PC_ABL == 4 && a_done)) {   // the next substep's A fragments (its half is the other one)
             if (j == 0) make_a(w0, 1, a10, a11);
             else if (j == 1) make_a(w1, 0, a00, a01);
             else make_a(w1, 1, a10, a11);
@@ -596,7 +599,7 @@ wq_horner_pc_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *
         full_step(sb, bF1, bF0, 3);
 #else
         read_bh(bP, sb, 0, 0);
-        make_a(w0, 0, a00, a01);
+        if (!(DLLM_PC_ABL == 4 && a_done)) make_a(w0, 0, a00, a01);
         half_step(sb, bP, bQ, 0, 0);
         half_step(sb, bQ, bP, 0, 1);
         half_step(sb, bP, bQ, 1, 0);
@@ -610,6 +613,7 @@ wq_horner_pc_kernel(const __half *__restrict__ X, int M, int K, const uint32_t *
         half_step(sb, bP, bQ, 3, 0);
         half_step(sb, bQ, bP, 3, 1);
 #endif
+        a_done = true;   // (DLLM_PC_ABL 4: A fragments built in the first stage only)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
