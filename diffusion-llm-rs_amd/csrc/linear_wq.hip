@@ -1426,13 +1426,20 @@ bool horner_pc_ready(const dllm_linear *hc, int M, hipStream_t st) {
 }
 
 // The two-k-group PC kernel (rows x 128 tiles, linear_pc.hip): where none of the larger Horner grids
-// fills a round, the largest rows in {128, 64} whose grid fills exactly one round (128: the 4-GPU
+// fills a round, 128- or 64-row tiles by rounds x tile time (below) (128: the 4-GPU
 // column shard M = 4096 x N 1024, M = 2048 x N 2048, M = 1024 x N 4096: 34.8 -> 32.3 us; 64: M = 512
 // x N 4096 and the 8-GPU shard 4096 x 512: 22.1 -> 21.5 us).  32-row tiles (DLLM_PC_KG2_SMALL, A/B)
 // lose to the 4-k-group fold tiles at mid M (M 256: 17.1 vs 14.3 us; profiles/r06_tiles/).  Returns
 // the tile rows, 0 = not applicable.
 #ifndef DLLM_HORNER_PC_KG2
 #define DLLM_HORNER_PC_KG2 1
+#endif
+// A 64-row grid of at least 3/4 of a round takes the two-k-group PC kernel: M 321..448 at N 4096
+// (192..224 tiles) ran 21.3 / 21.4 us at M 384 / 448 against 21.8 / 23.4 for the 4-k-group fold
+// tiles of mid M; at 5/8 of a round (M 300, 160 tiles) the fold tiles stay faster (21.4 vs 22.8 us;
+// profiles/r06_tiles/pc_kg2_fill_ab.jsonl, 40-layer chain).
+#ifndef DLLM_PC_KG2_MINFILL
+#define DLLM_PC_KG2_MINFILL (3 * kCUs / 4)
 #endif
 #ifndef DLLM_PC_KG2_SMALL   // 64- and 32-token tiles too
 #define DLLM_PC_KG2_SMALL 0
@@ -1448,12 +1455,25 @@ int horner_pc_kg2_rows(const dllm_linear *hc, int M, hipStream_t st) {
     if (hc->variant == 14 || hc->variant == 28) return 0;   // lab A/B: the fold-form exact policy
 #endif
     if (horner_ready(hc, M, st) || horner_pc_ready(hc, M, st) || horner_kg2_ready(hc, M)) return 0;
-    for (int rows = 128; rows >= (DLLM_PC_KG2_SMALL ? 32 : 64); rows /= 2) {
+#if DLLM_PC_KG2_SMALL
+    for (int rows = 128; rows >= 32; rows /= 2) {
         const int t = ((M + rows - 1) / rows) * (np / 128);
-        if (t >= 2 * kCUs) return 0;   // the next larger tile already had a full round
-        if (t >= kCUs) return rows;
+        if (t >= 2 * kCUs) return 0;
+        if (t >= DLLM_PC_KG2_MINFILL) return rows;
     }
     return 0;
+#else
+    // A 128-row tile takes ~1.55x a 64-row one (33 vs 21 us at K 4096: the 4- and 8-GPU shards), so
+    // a grid of 128-row tiles short of a round still beats two rounds of 64-row tiles, and a single
+    // round of 64-row tiles beats one of 128-row tiles.  N 4096: M 513..768 now take 128-row tiles
+    // (M 700 / 768: 42.1 / 39.1 -> 33.3 / 30.5 us in the 40-layer chain; they took 64-row tiles in
+    // 1.1 - 1.5 rounds) and M 321..448 64-row tiles (a 64-row grid of fewer than
+    // DLLM_PC_KG2_MINFILL tiles leaves mid M to the fold tiles); profiles/r06_tiles/pc_kg2_fill_ab.jsonl, pc_kg2_policy_ab.jsonl.
+    const int t128 = ((M + 127) / 128) * (np / 128), t64 = ((M + 63) / 64) * (np / 128);
+    if (t128 >= 2 * kCUs) return 0;   // the larger tiles of the other kernels fill the chip
+    if (t128 >= kCUs || t64 > kCUs) return 128;
+    return t64 >= DLLM_PC_KG2_MINFILL ? 64 : 0;
+#endif
 #else
     (void)hc; (void)M; (void)st;
     return 0;

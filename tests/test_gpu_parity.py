@@ -505,12 +505,14 @@ def test_linear_exact_weights_tight(dllm, torch, orc, M, N, group):
 @pytest.mark.parametrize("spread,M,K", [(8, 4096, 4096), (8, 8000, 1024), (8, 4300, 1024), (30, 4096, 2048), (45, 4096, 1024),
                                          (8, 1800, 4096), (30, 1850, 2048), (45, 1800, 1024),
                                          (8, 2048, 4096), (30, 3000, 2048), (45, 2048, 1024),
-                                         (8, 1024, 4096), (30, 1000, 2048), (45, 1024, 1024)])
+                                         (8, 1024, 4096), (30, 1000, 2048), (45, 1024, 1024),
+                                         (8, 448, 4096), (30, 400, 2048), (8, 700, 4096)])
 def test_linear_horner_scale_spread(dllm, torch, orc, spread, M, K):
     """The 256 x 256-tile exact kernel (int4 g128, >= 256 tiles) keeps one accumulator in Horner form:
     acc <- acc * (s_{g-1} / s_g) + T_g, times s_{G-1} at the end; at M = 2048 / 3000 the same form
     runs on the producer/consumer 128 x 256 tiles, at M = 1024 / 1000 on the two-k-group 128 x 128
-    producer/consumer tiles (one chain per K-half); at M = 1800 / 1850 (120 such tiles,
+    producer/consumer tiles (one chain per K-half), at M = 448 / 400 on their 64 x 128 form; at M =
+    1800 / 1850 (120 such tiles,
     240 of the fold form's 128 x 256) the 256 x 128-tile KG2 kernel runs one chain per K-half (the
     second starting from a zero accumulator) and sums the two halves' partials times their last
     scales.  Per-(group, column) weight
@@ -962,14 +964,17 @@ def test_linear_staggered_tiles_exact_integers(dllm, torch, K):
 
 @pytest.mark.parametrize("K", [256, 512, 768, 2304])
 @pytest.mark.parametrize("M,N", [(4096, 1024), (2048, 2048), (1024, 4096), (1000, 4096), (4096, 1020),
-                                 (512, 4096), (4096, 512), (500, 4096), (256, 4096), (300, 4096)])
+                                 (512, 4096), (4096, 512), (500, 4096), (256, 4096), (300, 4096),
+                                 (384, 4096), (420, 4096), (448, 4096), (576, 4096), (700, 4096)])
 def test_linear_pc_kg2_tiles_exact_integers(dllm, torch, K, M, N):
     """The two-k-group producer/consumer kernel (linear_pc.hip) on exact-integer data, bit-equal to
     the f64 product for f32 and f16 outputs: K-half kg's Horner chain in k-group kg, the halves'
     partials summed through LDS (each k-group finalizes half the token blocks).  Tiles of 128 x 128
     (the 4-GPU column shard 4096 x 1024, 2048 x 2048, 1024 x 4096) and 64 x 128 (M 512 / 500 at N
-    4096, the 8-GPU shard 4096 x 512); M 256 / 300 take the 4-k-group fold tiles of mid M (the
-    32 x 128 PC tiles are an A/B build only).  K 256 .. 2304 = 1 .. 9 groups
+    4096, the 8-GPU shard 4096 x 512, and M 384 / 420 / 448: grids of 3/4 of a round and more; M 576 /
+    700 take 128-row tiles short of a round rather than 64-row tiles in more than one); M
+    256 / 300 take the 4-k-group fold tiles of mid M (the 32 x 128 PC tiles are an A/B build only).
+    K 256 .. 2304 = 1 .. 9 groups
     per half (a ring period of 3 stages that does not divide the 2 .. 18 k-steps of a half); M
     1000 / 500 / 300 leave a ragged last row block, N 1020 a padded last column block (the 8-B
     row-store path)."""
