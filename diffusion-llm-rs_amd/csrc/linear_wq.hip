@@ -1355,6 +1355,16 @@ inline bool horner_shape(const dllm_linear *h) {
 // The handle's Horner ratios are valid (decided at create, immutable afterwards).
 inline bool ensure_horner(const dllm_linear *h, hipStream_t) { return h->hstate == 1; }
 
+// DLLM_POLICY_ROUNDS (product; 0 = the earlier full-round thresholds, A/B): a grid short of a round
+// takes the larger tiles when the alternative needs more rounds -- a 256 x 256 Horner round takes
+// about two 128 x 256 PC rounds, a 128 x 256 PC round about 1.78 two-k-group 128 x 128 rounds
+// (58.6 vs 33 us at K 4096).  N 4096, 40-layer chain (profiles/r06_tiles/policy_rounds_ab.jsonl):
+// M 1100 / 1280 / 1536 / 1800: 63.2 / 61.0 / 62.1 / 68.2 -> 56.8 / 52.3 / 53.2 / 59.0 us (128 x 256
+// PC tiles short of a round), M 2304 / 2560 / 3072 / 3584: 106.5 / 106.7 / 107.7 / 112.6 -> 97.3 /
+// 97.3 / 98.4 / 104.0 us (256 x 256 Horner tiles short of a round), M 2048 and 4096 unchanged.
+#ifndef DLLM_POLICY_ROUNDS
+#define DLLM_POLICY_ROUNDS 1
+#endif
 bool horner_ready(const dllm_linear *hc, int M, hipStream_t st) {
     const int np = static_cast<int>(hc->Npad);
     if (!horner_shape(hc)) return false;
@@ -1367,7 +1377,8 @@ bool horner_ready(const dllm_linear *hc, int M, hipStream_t st) {
         if (t128 < kCUs) return false;
     } else
 #endif
-    if (t256 < kCUs || 2 * ((t256 + kCUs - 1) / kCUs) > (t128 + kCUs - 1) / kCUs) return false;
+    if ((!DLLM_POLICY_ROUNDS && t256 < kCUs) || 2 * ((t256 + kCUs - 1) / kCUs) > (t128 + kCUs - 1) / kCUs)
+        return false;
     return ensure_horner(hc, st);
 }
 
@@ -1418,7 +1429,11 @@ bool horner_pc_ready(const dllm_linear *hc, int M, hipStream_t st) {
     if (hc->variant == 14 || hc->variant == 28) return false;   // lab A/B: the fold-form exact policy
 #endif
     const int t128 = ((M + 127) / 128) * (np / 256);
-    return t128 >= kCUs && !horner_ready(hc, M, st);
+    if (horner_ready(hc, M, st)) return false;
+    if (t128 >= kCUs) return true;
+    if (!DLLM_POLICY_ROUNDS || np % 128 != 0 || hc->K % 256 != 0) return false;
+    const int tk = ((M + 127) / 128) * (np / 128);   // the two-k-group 128 x 128 grid
+    return 178 * ((t128 + kCUs - 1) / kCUs) <= 100 * ((tk + kCUs - 1) / kCUs);
 #else
     (void)hc; (void)M; (void)st;
     return false;
