@@ -1055,6 +1055,11 @@ int launch_exact_tile(const ExactGemmArgs &a, int nsplit, hipStream_t st) {
 // us, profiles/r03_midm/ring_depth.jsonl): the single wave per SIMD is issue/latency bound, not
 // fed short of bytes.
 constexpr int kMidRing = 3;
+// The mid-M tiles also where their grid is short of a round (DLLM_MIDM_MINFILL tiles and more): one
+// 32 x 128 tile per CU takes the same time whether 96 or 256 CUs have one.
+#ifndef DLLM_MIDM_MINFILL
+#define DLLM_MIDM_MINFILL 96
+#endif
 
 template <int BITS, typename YT, int G64, int EPI>
 int launch_exact_bits(const ExactGemmArgs &a, hipStream_t st) {
@@ -1093,7 +1098,7 @@ int launch_exact_bits(const ExactGemmArgs &a, hipStream_t st) {
     // (profiles/r03_midm/policy_ab.json).
     if constexpr (G64 == 2 && BITS == 4 && DLLM_EXACT_WREG) {
         const int t32 = ((a.M + 31) / 32) * (a.Npad / 128), t64 = ((a.M + 63) / 64) * (a.Npad / 128);
-        if (a.lab_policy != 1 && tiles < kCUs && t64 < kCUs && t32 >= kCUs) {
+        if (a.lab_policy != 1 && tiles < kCUs && t64 < kCUs && t32 >= DLLM_MIDM_MINFILL) {
 #if DLLM_LAB
             switch (a.lab_policy) {   // lab A/B: one k-group (RING 3) / two k-groups / four (RING 3)
             case 2: return launch_exact_tile<BITS, YT, 4, 1, 2, 1, EPI, false, 1, kMidRing>(a, 1, st);

@@ -448,7 +448,8 @@ def test_linear_split_k_exact_integers(dllm, torch, orc):
 @pytest.mark.parametrize("precision", [0, 1])
 @pytest.mark.parametrize("bits", [2, 4, 8])
 @pytest.mark.parametrize("M,N", [(4096, 4096), (2048, 4096), (1800, 4096), (4096, 1024), (4096, 512), (512, 1024),
-                                 (300, 256), (64, 200), (33, 200), (17, 200), (1, 200), (4096, 4092), (2048, 4092)])
+                                 (300, 256), (64, 200), (33, 200), (17, 200), (1, 200), (4096, 4092), (2048, 4092),
+                                 (128, 4096), (200, 4096)])
 def test_linear_policy_exact_integers(dllm, torch, orc, precision, bits, M, N):
     """Every tile of both precision policies on exact-integer data (each group spans [0, 2^b - 1]:
     scale 1, zp 0; K = 768 = 6 groups, so every product and partial sum is an exact integer):
@@ -480,7 +481,8 @@ def test_linear_policy_exact_integers(dllm, torch, orc, precision, bits, M, N):
 
 @pytest.mark.parametrize("M,N,group", [(4096, 4096, 128), (2048, 4096, 128), (2048, 4096, 64), (2048, 4096, 256),
                                        (4096, 2048, 128), (3001, 4096, 128), (4096, 1024, 128), (4096, 512, 128), (256, 4096, 128), (65, 4096, 256),
-                                       (64, 4096, 128), (40, 1024, 64), (16, 4096, 128), (1, 4096, 256)])
+                                       (64, 4096, 128), (40, 1024, 64), (16, 4096, 128), (1, 4096, 256),
+                                       (128, 4096, 128), (200, 4096, 128)])
 def test_linear_exact_weights_tight(dllm, torch, orc, M, N, group):
     """DLLM_PRECISION_EXACT: the MFMA consumes the exact integer (q - zp) and the f32 scale is
     applied per group, so against the f32 product of the same f16-rounded X with the reference's
