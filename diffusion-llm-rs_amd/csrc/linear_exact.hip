@@ -1056,7 +1056,9 @@ int launch_exact_tile(const ExactGemmArgs &a, int nsplit, hipStream_t st) {
 // fed short of bytes.
 constexpr int kMidRing = 3;
 // The mid-M tiles also where their grid is short of a round (DLLM_MIDM_MINFILL tiles and more): one
-// 32 x 128 tile per CU takes the same time whether 96 or 256 CUs have one.
+// 32 x 128 tile per CU takes the same time whether 96 or 256 CUs have one.  N 4096, 40-layer chain:
+// M 65 / 96 / 128 / 160 / 192 / 224 = 16.5 / 18.2 / 20.4 / 23.1 / 24.6 / 23.5 -> 15.4 / 17.2 / 17.1 /
+// 16.5 / 16.6 / 16.5 us against the K-split 64 x 128 tiles (profiles/r06_tiles/midm_short_grid_ab.jsonl).
 #ifndef DLLM_MIDM_MINFILL
 #define DLLM_MIDM_MINFILL 96
 #endif
