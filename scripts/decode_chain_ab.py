@@ -11,9 +11,9 @@ import sys, json, time, torch
 sys.path.insert(0, %r)
 import __graft_entry__ as g
 d = g.load_package(); import scripts._lab as _lab; _lab.select(d)
-K = N = 4096
 gen = torch.Generator(device="cuda").manual_seed(99)
 import os
+K = 4096; N = int(os.environ.get("AB_N", "4096"))
 po = os.environ.get("PO") == "1"   # prefill-only handles: M <= 64 runs the exact prefill kernels
 chain = [d.QuantLinear.from_weight(0.02 * torch.randn(K, N, device="cuda", generator=gen), None, 4, 128, prefill_only=po) for _ in range(40)]
 out = {}
