@@ -1058,9 +1058,11 @@ constexpr int kMidRing = 3;
 // The mid-M tiles also where their grid is short of a round (DLLM_MIDM_MINFILL tiles and more): one
 // 32 x 128 tile per CU takes the same time whether 96 or 256 CUs have one.  N 4096, 40-layer chain:
 // M 65 / 96 / 128 / 160 / 192 / 224 = 16.5 / 18.2 / 20.4 / 23.1 / 24.6 / 23.5 -> 15.4 / 17.2 / 17.1 /
-// 16.5 / 16.6 / 16.5 us against the K-split 64 x 128 tiles (profiles/r06_tiles/midm_short_grid_ab.jsonl).
+// 16.5 / 16.6 / 16.5 us against the K-split 64 x 128 tiles (profiles/r06_tiles/midm_short_grid_ab.jsonl);
+// from 48 tiles (narrow N): N 2048 M 128 15.0 -> 13.2, N 1024 M 256 14.9 -> 13.2, N 512 M 384 / 512
+// 13.7 / 15.0 -> 13.2 / 13.2 us, nothing slower (profiles/r06_tiles/m48/).
 #ifndef DLLM_MIDM_MINFILL
-#define DLLM_MIDM_MINFILL 96
+#define DLLM_MIDM_MINFILL 48
 #endif
 
 template <int BITS, typename YT, int G64, int EPI>
